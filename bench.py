@@ -1,0 +1,218 @@
+"""Benchmark: pivots/s of the dense fp64 tableau simplex on MI355X.
+
+A "step" is one pivot (entering scan + ratio test + pivot-row normalise +
+Gauss-Jordan elimination of the whole tableau) of BASELINE.json config 3:
+an 8192 x 16384 dense random-feasible LP, tableau 8193 x 16385 fp64 (1.07 GB)
+resident in HBM before timing starts.  With --gpus N > 1 (launched by
+torch.distributed.run, one process per GPU) the SAME tableau is row-sharded
+across the N GPUs (config 4): strong scaling, value = whole-job pivots/s.
+
+Output: ONE JSON line on rank 0 (contract in the task statement), with
+`roofline` for the elimination kernel (HIP-event timed inside the timed
+region; algorithmic bytes = 16 B per touched tableau element)
+and `cpu_baseline` (the numpy oracle on a bounded sample of the same
+workload, 1 thread, rank 0 at N=1 only).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "simplex-solver_amd"))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+
+METRIC = "pivots/sec + row-elim HBM GB/s (% roofline), fp64 dense tableau, 1/2/4/8 GPU"
+HBM_PEAK_GBPS = 8000.0  # MI355X spec HBM3E peak (MI355X_MICROARCH.md)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=500)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--m", type=int, default=8192)
+    ap.add_argument("--n", type=int, default=8192)
+    ap.add_argument("--seed", type=int, default=20251205)
+    ap.add_argument("--rule", default="dantzig")
+    ap.add_argument("--dense", action="store_true", help="dense sweep (no zero-column skip)")
+    ap.add_argument("--nt", action="store_true", help="non-temporal elimination stream")
+    ap.add_argument("--graph", type=int, default=-1,
+                    help="1: time hipGraph replays (elim events in a separate window); "
+                         "0: direct launches with per-elim events; -1: auto (N>1 -> 1)")
+    ap.add_argument("--cpu-seconds", type=float, default=15.0,
+                    help="budget of the CPU-baseline sample (0 disables)")
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles",
+                                                           "traffic_r01.json"))
+    return ap.parse_args()
+
+
+def dist_env():
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", str(rank)))
+    return world, rank, local
+
+
+def cpu_baseline(m, n, seed, rule, budget_s, gpu_hist):
+    """Time the numpy oracle on the same tableau (rank 0, N=1)."""
+    from oracle import simplex_oracle as O
+    from simplex_amd import synth
+    Tf, obj, basis = synth.tableau_rows("dense", m, n, seed, order="C")
+    T = np.vstack([Tf, obj[None, :]])
+    del Tf
+    k, t0 = 0, time.perf_counter()
+    hist = []
+    while time.perf_counter() - t0 < budget_s and k < 2000:
+        c = O.select_entering(T[-1], T.shape[1] - 1, rule, 1e-9)
+        r = O.ratio_test(T, c, basis, rule, 1e-12)
+        O.pivot(T, r, c)
+        basis[r] = c
+        hist.append((r, c))
+        k += 1
+    el = time.perf_counter() - t0
+    match = [tuple(h) for h in gpu_hist[:k]] == hist
+    return {"value": k / el, "unit": "pivots/s", "cores": 1, "kind": "port",
+            "sample": f"numpy oracle (oracle/simplex_oracle.py), first {k} {rule} pivots of the "
+                      f"same {m}x{n} tableau from the slack basis, {el:.1f} s, 1 thread",
+            "pivot_sequence_matches_gpu": bool(match),
+            "host": {"cpu_count": os.cpu_count(),
+                     "OMP_NUM_THREADS": os.environ.get("OMP_NUM_THREADS"),
+                     "model": _cpu_model()}}
+
+
+def _cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
+
+
+def main():
+    args = parse()
+    world, rank, local = dist_env()
+    if args.gpus != world and world > 1:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE {world}")
+    use_graph = (world > 1) if args.graph < 0 else bool(args.graph)
+
+    import torch  # device discovery / distributed plumbing only
+    import torch.distributed as tdist
+    from simplex_amd import synth
+    from simplex_amd.dist import ShardedTableau, exchange_unique_id, row_partition
+    from simplex_amd.engine import DeviceTableau
+
+    if not torch.cuda.is_available():
+        raise SystemExit("bench.py needs a GPU (HIP); none visible")
+    m, n = args.m, args.n
+    if world > 1:
+        tdist.init_process_group("gloo")
+        uid = exchange_unique_id()
+        eng = ShardedTableau(local, rank, world, uid)
+    else:
+        eng = DeviceTableau(0)
+    row0, row1 = row_partition(m, world, rank)
+    Tf, obj, basis = synth.tableau_rows("dense", m, n, args.seed, row0, row1, order="F")
+    eng.load_rows(Tf, obj, basis, m, row0)
+    del Tf
+    eng.set_elim_nt(args.nt)
+    opts = dict(rule=args.rule, skip_zero_cols=not args.dense, use_graph=True, chunk=32)
+
+    def barrier():
+        if world > 1:
+            tdist.barrier()
+
+    eng.run_pivots(args.warmup, **opts)
+    eng.sync()
+    eng.elim_timing(reset=True)
+    barrier()
+    eng.sync()
+    t0 = time.perf_counter()
+    eng.run_pivots(args.steps, time_elim=not use_graph, **opts)
+    eng.sync()
+    t1 = time.perf_counter()
+    barrier()
+    elapsed = t1 - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    status, iters, z = eng.state()
+    if status != 4 or iters != args.warmup + args.steps:
+        raise SystemExit(f"pivot loop ended early: status {status}, iters {iters}")
+    ms_tot, launches, touched = eng.elim_timing(reset=True)
+    window = "timed region (per-launch HIP events on the engine stream)"
+    if use_graph or launches == 0:
+        eng.run_pivots(64, time_elim=True, **opts)
+        eng.sync()
+        ms_tot, launches, touched = eng.elim_timing(reset=True)
+        window = "64-pivot event window right after the graph-timed region"
+    avg_ms = ms_tot / launches
+    m_local = row1 - row0
+    N = n + m + 1
+    cols_per_launch = touched / launches
+    # algorithmic HBM bytes of one elimination launch: read+write 16 B for every
+    # touched element except the entering column, which is only written (8 B)
+    alg_bytes = 16.0 * m_local * (cols_per_launch - 1.0) + 8.0 * m_local
+    dense_bytes = 16.0 * (m_local + 1) * N  # SURVEY §8(d) per-pivot figure (no skip)
+    achieved = alg_bytes / (avg_ms * 1e-3) / 1e9
+    traffic = None
+    try:
+        tj = json.load(open(args.traffic_json))
+        key = f"{m}x{n}_w{world}_{'dense' if args.dense else 'skip'}"
+        traffic = tj.get(key, {}).get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        pass
+
+    hist = eng.history() if (rank == 0 and world == 1 and args.cpu_seconds > 0) else None
+    cpu = None
+    if hist is not None:
+        cpu = cpu_baseline(m, n, args.seed, args.rule, args.cpu_seconds, hist.tolist())
+    if rank == 0:
+        value = args.steps / elapsed
+        line = {
+            "metric": METRIC,
+            "value": value,
+            "unit": "pivots/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": 1e3 * elapsed / args.steps,
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": f"synthetic: hash-seeded dense random-feasible LP (simplex_amd.synth, "
+                    f"seed {args.seed})",
+            "config": {"workload": ("config 3: 8192x16384 fp64 dense tableau" if world == 1
+                                    else f"config 4: config-3 tableau row-sharded x{world}"),
+                       "m": m, "n": n, "tableau": [m + 1, N], "rule": args.rule,
+                       "elimination": "dense sweep" if args.dense else "skip p[j]==0 columns",
+                       "timing": "hipGraph replay" if use_graph else "direct launches",
+                       "parallelism": f"row-shard x{world}" if world > 1 else "single GPU"},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS,
+                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBPS,
+                         "traffic": traffic, "kernel": "spx::elim_kernel",
+                         "avg_launch_us": avg_ms * 1e3,
+                         "alg_bytes_per_launch": alg_bytes,
+                         "touched_cols_per_launch": cols_per_launch,
+                         "dense_equiv_GBps": dense_bytes / (avg_ms * 1e-3) / 1e9,
+                         "window": window},
+            "cpu_baseline": cpu,
+            "objective_after": z,
+        }
+        print(json.dumps(line), flush=True)
+    eng.close()
+    if world > 1:
+        tdist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

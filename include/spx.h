@@ -1,0 +1,159 @@
+/*
+ * spx.h — C-ABI of the MI355X dense simplex pivot engine (libspx.so).
+ *
+ * This is the drop-in boundary for the tableau-pivoting hot path of
+ * the-utn-team/simplex-solver.  In the reference that path is the third-party
+ * `simple_simplex==0.0.3` engine, driven from
+ *   app/controllers/solver_controller.py:290-319  (_run_simple_simplex:
+ *       create_tableau / add_constraint / add_objective / optimize_json_format)
+ * and its pivot history is consumed at solver_controller.py:322-363.
+ * The Python module `simplex_amd.simple_simplex` re-exposes those four names on
+ * top of the entry points below (binding: simplex_amd/_lib.py).
+ *
+ * Conventions
+ *  - Plain pointers and sizes only; no torch types.
+ *  - The caller owns every host buffer; the library copies in/out and never
+ *    keeps a host pointer after a call returns.  A context owns all device
+ *    memory (and the RCCL communicator of a sharded context); spx_destroy
+ *    frees it.
+ *  - Re-entrant: no global mutable state.  One context per solve, one HIP
+ *    stream per context; distinct contexts may be used from distinct threads
+ *    concurrently (the reference's /solve is entered from many threads,
+ *    tests/test_performance_load.py:80-83).
+ *  - Tableau (the spec): rows 0..m-1 are constraints, the
+ *    objective row is logically row m ("z_j - c_j" form of a MAX problem, RHS
+ *    = current objective value).  Columns 0..N-2 are variables, column N-1 is
+ *    the right-hand side.  basis[i] = index of the variable basic in row i.
+ *  - Return codes: >= 0 is a solve status with the same numbering as scipy's
+ *    OptimizeResult.status (which solver_controller.py:404 maps):
+ *       SPX_OPTIMAL 0, SPX_ITER_LIMIT 1, SPX_INFEASIBLE 2, SPX_UNBOUNDED 3;
+ *    plain calls return SPX_OK (0).  Negative values are errors; the message
+ *    is available from spx_last_error(ctx).
+ */
+#ifndef SPX_H_
+#define SPX_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SPX_ABI_VERSION 1
+
+/* status / return codes */
+#define SPX_OK 0
+#define SPX_OPTIMAL 0
+#define SPX_ITER_LIMIT 1
+#define SPX_INFEASIBLE 2
+#define SPX_UNBOUNDED 3
+#define SPX_RUNNING 4 /* spx_pivot: a pivot was made, not finished */
+#define SPX_E_ARG (-1)
+#define SPX_E_HIP (-2)
+#define SPX_E_RCCL (-3)
+#define SPX_E_STATE (-4)
+#define SPX_E_OOM (-5)
+
+/* pivot rules */
+#define SPX_RULE_DANTZIG 0 /* most negative reduced cost, lowest column on ties; lowest row on ratio ties */
+#define SPX_RULE_BLAND 1   /* lowest column with rc < -eps_opt; lowest basic-variable index on ratio ties */
+
+/* layouts of host tableau buffers */
+#define SPX_ROW_MAJOR 0 /* element (i,j) at buf[i*ld + j] */
+#define SPX_COL_MAJOR 1 /* element (i,j) at buf[j*ld + i] */
+
+typedef struct spx_ctx spx_ctx;
+
+typedef struct spx_opts {
+  int32_t rule;          /* SPX_RULE_* */
+  int32_t skip_zero_cols;/* 1 (default): columns with p[j]==0 are left untouched (bit-identical
+                            to the dense update up to the sign of zero); 0: dense sweep */
+  double eps_opt;        /* optimality tolerance on reduced costs (default 1e-9) */
+  double eps_piv;        /* minimum pivot-column entry for the ratio test (default 1e-12) */
+  int64_t max_iters;     /* pivots allowed in this call (<=0: unlimited) */
+  double time_limit_s;   /* wall-clock limit (<=0: none); checked between pivot chunks */
+  int64_t n_enter;       /* columns [0, n_enter) may enter; <=0 means all but the RHS */
+  int32_t chunk;         /* pivots per hipGraph replay (<=0: default 32) */
+  int32_t use_graph;     /* 1 (default): replay captured pivot chunks; 0: direct launches */
+} spx_opts;
+
+typedef struct spx_result {
+  int32_t status;        /* SPX_OPTIMAL / SPX_ITER_LIMIT / SPX_UNBOUNDED */
+  int32_t pad;
+  int64_t iters;         /* pivots made by this call */
+  double objective;      /* tableau objective-row RHS (value of the MAX form) */
+  double elapsed_s;      /* wall time of the call */
+} spx_result;
+
+/* Fill *o with the defaults documented above. */
+void spx_default_opts(spx_opts* o);
+
+/* ---- context lifetime ---------------------------------------------------- */
+int spx_create(spx_ctx** out, int device);
+int spx_destroy(spx_ctx* ctx);
+const char* spx_last_error(const spx_ctx* ctx);
+int spx_abi_version(void);
+
+/* ---- sharded (multi-GPU) contexts: one process per GPU, RCCL over xGMI ---- */
+/* Writes the 128-byte RCCL unique id (rank 0 creates it; the caller ships it
+ * to the other ranks, e.g. with torch.distributed over gloo/TCP). */
+int spx_comm_unique_id(char out_id[128]);
+/* Like spx_create, but joins a communicator of nranks contexts; rank r will
+ * own a contiguous block of constraint rows (given at load time). */
+int spx_create_sharded(spx_ctx** out, int device, int rank, int nranks, const char id[128]);
+
+/* ---- data in / out ------------------------------------------------------- */
+/* Load a full tableau of `rows` = m+1 rows (objective row LAST) and `cols` = N
+ * columns; basis has m entries.  ld is the host leading dimension. */
+int spx_load(spx_ctx* ctx, const double* T, int64_t rows, int64_t cols, int64_t ld,
+             int layout, const int64_t* basis);
+/* Sharded load: this rank's constraint rows [row0, row0+m_local) of a tableau
+ * with m_global constraint rows, the (replicated) objective row `obj` (N
+ * values) and the full basis (m_global entries).  Also valid for 1 rank. */
+int spx_load_rows(spx_ctx* ctx, const double* A, int64_t m_local, int64_t cols, int64_t ld,
+                  int layout, const double* obj, const int64_t* basis, int64_t m_global,
+                  int64_t row0);
+/* Replace the objective row (N values), e.g. between phase 1 and phase 2. */
+int spx_set_objective(spx_ctx* ctx, const double* obj);
+/* Copy out this context's rows (m_local+1 rows, objective row last). */
+int spx_get_tableau(spx_ctx* ctx, double* out, int64_t ld, int layout);
+int spx_get_objective(spx_ctx* ctx, double* out);      /* N values */
+int spx_get_basis(spx_ctx* ctx, int64_t* out);         /* m_global values */
+int spx_get_column(spx_ctx* ctx, int64_t j, double* out); /* local rows of column j */
+/* Pivot history of the context since load: up to `cap` (row, col) pairs,
+ * returns the number of pivots recorded in *n. */
+int spx_get_history(spx_ctx* ctx, int64_t* rc_pairs, int64_t cap, int64_t* n);
+int spx_dims(const spx_ctx* ctx, int64_t* m_global, int64_t* m_local, int64_t* cols,
+             int64_t* row0);
+
+/* ---- pivoting ------------------------------------------------------------ */
+/* Run the pivot loop until optimal / unbounded / limits. */
+int spx_solve(spx_ctx* ctx, const spx_opts* opts, spx_result* res);
+/* One pivot chosen by the rule.  Returns SPX_RUNNING with *r,*c set when a
+ * pivot was made, or SPX_OPTIMAL / SPX_UNBOUNDED (no pivot made). */
+int spx_pivot(spx_ctx* ctx, const spx_opts* opts, int64_t* r, int64_t* c);
+/* One pivot on a given element (r, c) (used to drive artificial variables out
+ * of the basis after phase 1).  T[r,c] must be nonzero. */
+int spx_pivot_at(spx_ctx* ctx, int64_t r, int64_t c);
+/* Enqueue exactly `npivots` rule-chosen pivots without host synchronisation
+ * (benchmark primitive; pivots after termination are no-ops on the device).
+ * If `time_elim` is nonzero, HIP events bracket every elimination launch. */
+int spx_run_pivots(spx_ctx* ctx, const spx_opts* opts, int64_t npivots, int time_elim);
+int spx_sync(spx_ctx* ctx);
+/* Device-side state after spx_sync: status code (SPX_RUNNING while going),
+ * total pivots since load, and the objective-row RHS. */
+int spx_state(spx_ctx* ctx, int32_t* status, int64_t* iters, double* objective);
+/* Sum and count of the elimination-kernel event timings collected by
+ * spx_run_pivots(..., time_elim=1) since the last reset; `touched_cols`
+ * receives the sum over those pivots of the number of columns the kernel
+ * updated (for algorithmic-byte accounting). */
+int spx_elim_timing(spx_ctx* ctx, double* total_ms, int64_t* count, int64_t* touched_cols,
+                    int reset);
+
+/* Tuning knob: 1 = non-temporal loads/stores in the elimination stream. */
+int spx_set_elim_nt(spx_ctx* ctx, int nt);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SPX_H_ */

@@ -1,0 +1,709 @@
+// spx_capi.hip — C-ABI of the MI355X simplex pivot engine (declared in include/spx.h).
+//
+// Host runtime: one context = one HIP stream + the device-resident tableau,
+// pivot vectors, reduction partials and a device State block.  The pivot loop
+// never round-trips to the host inside a chunk: each pivot is three kernels
+// (ratio -> norm -> elim), and chunks of `chunk` pivots are captured once into
+// a hipGraph and replayed; the host only reads the 80-byte State (pinned) after
+// each chunk to check for termination / limits.
+//
+// Sharded contexts (spx_create_sharded) split the constraint rows across ranks,
+// one process per GPU.  Per pivot they add one RCCL all-gather of a 32-B
+// leaving-row candidate per rank (the "allreduce-min" of the leaving row:
+// every rank reduces the gathered keys identically) and one RCCL all-reduce
+// of the pivot row (the broadcast from the owner rank, done as a sum with zeros
+// elsewhere so the root never has to be known on the host).
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/spx.h"
+#include "spx_kernels.hpp"
+
+using namespace spx;
+
+struct spx_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  std::string err;
+
+  // distribution
+  int rank = 0, nranks = 1;
+  bool sharded = false;
+  ncclComm_t comm = nullptr;
+
+  // dims
+  int64_t m_global = 0, m_local = 0, row0 = 0, N = 0, ld = 0;
+  bool loaded = false;
+
+  // device buffers
+  double* A = nullptr;     // ld * N, column-major local rows
+  double* obj = nullptr;   // N
+  double* F = nullptr;     // ld   pivot-column snapshot
+  double* P = nullptr;     // N    pivot row (normalised)
+  int* list = nullptr;     // N    compacted columns
+  int64_t* basis = nullptr;// m_global
+  int64_t* hist = nullptr; // 2 * hist_cap
+  Key* enter_part = nullptr;
+  Key* ratio_part = nullptr;
+  Key* sendkey = nullptr;
+  Key* keys_all = nullptr;
+  Params* prm = nullptr;
+  State* st = nullptr;
+  State* h_st = nullptr;   // pinned mirror
+  int64_t hist_cap = 0;
+
+  // launch geometry
+  int nbn = 1, nbr = 1, rch = 1, G = 1, R = 8;
+  int elim_nt = 0;
+
+  // graph cache
+  hipGraphExec_t gexec = nullptr;
+  int gchunk = 0;
+
+  // elimination timing
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> ev;
+  size_t ev_used = 0;
+  int64_t touched_at_reset = 0;
+};
+
+namespace {
+
+#define HIPC(expr)                                                                  \
+  do {                                                                              \
+    hipError_t e_ = (expr);                                                         \
+    if (e_ != hipSuccess) {                                                         \
+      ctx->err = std::string(#expr) + ": " + hipGetErrorString(e_);                 \
+      return SPX_E_HIP;                                                             \
+    }                                                                               \
+  } while (0)
+
+#define NCCLC(expr)                                                                 \
+  do {                                                                              \
+    ncclResult_t e_ = (expr);                                                       \
+    if (e_ != ncclSuccess) {                                                        \
+      ctx->err = std::string(#expr) + ": " + ncclGetErrorString(e_);                \
+      return SPX_E_RCCL;                                                            \
+    }                                                                               \
+  } while (0)
+
+#define CHECK_ARG(cond, msg)                                                        \
+  do {                                                                              \
+    if (!(cond)) {                                                                  \
+      ctx->err = (msg);                                                             \
+      return SPX_E_ARG;                                                             \
+    }                                                                               \
+  } while (0)
+
+template <typename T>
+void dfree(T*& p) {
+  if (p) (void)hipFree(p);
+  p = nullptr;
+}
+
+int free_buffers(spx_ctx* ctx) {
+  if (ctx->gexec) (void)hipGraphExecDestroy(ctx->gexec);
+  ctx->gexec = nullptr;
+  ctx->gchunk = 0;
+  dfree(ctx->A);
+  dfree(ctx->obj);
+  dfree(ctx->F);
+  dfree(ctx->P);
+  dfree(ctx->list);
+  dfree(ctx->basis);
+  dfree(ctx->hist);
+  dfree(ctx->enter_part);
+  dfree(ctx->ratio_part);
+  dfree(ctx->sendkey);
+  dfree(ctx->keys_all);
+  ctx->loaded = false;
+  return SPX_OK;
+}
+
+int64_t round_up(int64_t x, int64_t a) { return (x + a - 1) / a * a; }
+
+// Elimination geometry: rows per thread R, row chunks rch, column groups G.
+void choose_geometry(spx_ctx* ctx) {
+  const int64_t m = ctx->m_local;
+  ctx->R = (m >= 4096) ? 8 : (m >= 1024 ? 4 : 2);
+  const int64_t rc = (int64_t)BLK * ctx->R;
+  ctx->rch = (int)std::max<int64_t>(1, (m + rc - 1) / rc);
+  const int target = 2048;  // 256 CUs x 8 workgroups
+  ctx->G = std::max(1, target / ctx->rch);
+  ctx->G = (int)std::min<int64_t>(ctx->G, std::max<int64_t>(1, ctx->N));
+  ctx->nbn = (int)std::max<int64_t>(1, (ctx->N + BLK - 1) / BLK);
+  ctx->nbr = (int)std::min<int64_t>(256, std::max<int64_t>(1, (m + 2 * BLK - 1) / (2 * BLK)));
+}
+
+template <int R, bool NT>
+void launch_elim_t(spx_ctx* ctx) {
+  hipLaunchKernelGGL((elim_kernel<R, NT>), dim3(ctx->rch * ctx->G), dim3(BLK), 0, ctx->stream,
+                     ctx->A, ctx->ld, ctx->m_local, ctx->row0, ctx->F, ctx->P, ctx->list,
+                     ctx->rch, ctx->G, ctx->st);
+}
+
+void launch_elim(spx_ctx* ctx) {
+  const bool nt = ctx->elim_nt != 0;
+  switch (ctx->R) {
+    case 8: nt ? launch_elim_t<8, true>(ctx) : launch_elim_t<8, false>(ctx); break;
+    case 4: nt ? launch_elim_t<4, true>(ctx) : launch_elim_t<4, false>(ctx); break;
+    default: nt ? launch_elim_t<2, true>(ctx) : launch_elim_t<2, false>(ctx); break;
+  }
+}
+
+template <int MODE>
+void launch_norm(spx_ctx* ctx, const Key* keys, int nkeys) {
+  hipLaunchKernelGGL((norm_kernel<MODE>), dim3(ctx->nbn), dim3(BLK), 0, ctx->stream, ctx->A,
+                     ctx->ld, ctx->m_local, ctx->row0, ctx->N, ctx->obj, ctx->F, ctx->P,
+                     ctx->list, keys, nkeys, ctx->enter_part, ctx->basis, ctx->hist, ctx->prm,
+                     ctx->st);
+}
+
+void launch_ratio(spx_ctx* ctx) {
+  hipLaunchKernelGGL(ratio_kernel, dim3(ctx->nbr), dim3(BLK), 0, ctx->stream, ctx->A, ctx->ld,
+                     ctx->m_local, ctx->row0, ctx->N, ctx->obj, ctx->F, ctx->enter_part,
+                     ctx->nbn, ctx->ratio_part, ctx->basis, ctx->prm, ctx->st);
+}
+
+// Enqueue one pivot (all launches on ctx->stream; no host synchronisation).
+int enqueue_pivot(spx_ctx* ctx, bool time_elim) {
+  launch_ratio(ctx);
+  if (!ctx->sharded) {
+    launch_norm<MODE_FUSED>(ctx, ctx->ratio_part, ctx->nbr);
+  } else {
+    hipLaunchKernelGGL(select_kernel, dim3(1), dim3(BLK), 0, ctx->stream, ctx->ratio_part,
+                       ctx->nbr, ctx->sendkey, ctx->st);
+    NCCLC(ncclAllGather(ctx->sendkey, ctx->keys_all, sizeof(Key), ncclUint8, ctx->comm,
+                        ctx->stream));
+    launch_norm<MODE_PROW>(ctx, ctx->keys_all, ctx->nranks);
+    NCCLC(ncclAllReduce(ctx->P, ctx->P, (size_t)ctx->N, ncclDouble, ncclSum, ctx->comm,
+                        ctx->stream));
+    launch_norm<MODE_FINISH>(ctx, nullptr, 0);
+  }
+  if (time_elim) {
+    if (ctx->ev_used == ctx->ev.size()) {
+      hipEvent_t a, b;
+      HIPC(hipEventCreate(&a));
+      HIPC(hipEventCreate(&b));
+      ctx->ev.emplace_back(a, b);
+    }
+    auto& e = ctx->ev[ctx->ev_used++];
+    HIPC(hipEventRecord(e.first, ctx->stream));
+    launch_elim(ctx);
+    HIPC(hipEventRecord(e.second, ctx->stream));
+  } else {
+    launch_elim(ctx);
+  }
+  HIPC(hipGetLastError());
+  return SPX_OK;
+}
+
+int write_params(spx_ctx* ctx, const spx_opts* o) {
+  spx_opts d;
+  spx_default_opts(&d);
+  if (!o) o = &d;
+  CHECK_ARG(o->rule == SPX_RULE_DANTZIG || o->rule == SPX_RULE_BLAND, "unknown pivot rule");
+  Params p;
+  p.rule = o->rule;
+  p.skip_zero = o->skip_zero_cols ? 1 : 0;
+  p.eps_opt = o->eps_opt;
+  p.eps_piv = o->eps_piv;
+  p.n_enter = (o->n_enter > 0) ? std::min<int64_t>(o->n_enter, ctx->N - 1) : ctx->N - 1;
+  p.iter_limit = (o->max_iters > 0) ? ctx->h_st->iters + o->max_iters : INT64_MAX;
+  HIPC(hipMemcpyAsync(ctx->prm, &p, sizeof(p), hipMemcpyHostToDevice, ctx->stream));
+  return SPX_OK;
+}
+
+// Host-side writes of State fields (synchronous; between pivot calls only).
+int set_state_fields(spx_ctx* ctx, int32_t status, int64_t fc, int64_t fr) {
+  ctx->h_st->status = status;
+  ctx->h_st->forced_c = fc;
+  ctx->h_st->forced_r = fr;
+  HIPC(hipMemcpyAsync(ctx->st, ctx->h_st, sizeof(State), hipMemcpyHostToDevice, ctx->stream));
+  return SPX_OK;
+}
+
+int pull_state(spx_ctx* ctx) {
+  HIPC(hipMemcpyAsync(ctx->h_st, ctx->st, sizeof(State), hipMemcpyDeviceToHost, ctx->stream));
+  HIPC(hipStreamSynchronize(ctx->stream));
+  return SPX_OK;
+}
+
+// Prepare a pivot call: params, status RUNNING, fresh entering partials.
+int begin_call(spx_ctx* ctx, const spx_opts* o) {
+  if (!ctx->loaded) {
+    ctx->err = "no tableau loaded";
+    return SPX_E_STATE;
+  }
+  int rc = pull_state(ctx);
+  if (rc) return rc;
+  if ((rc = write_params(ctx, o))) return rc;
+  if ((rc = set_state_fields(ctx, ST_RUNNING, -1, -1))) return rc;
+  launch_norm<MODE_INIT>(ctx, nullptr, 0);
+  HIPC(hipGetLastError());
+  return SPX_OK;
+}
+
+int build_graph(spx_ctx* ctx, int chunk) {
+  if (ctx->gexec && ctx->gchunk == chunk) return SPX_OK;
+  if (ctx->gexec) (void)hipGraphExecDestroy(ctx->gexec);
+  ctx->gexec = nullptr;
+  hipGraph_t g = nullptr;
+  HIPC(hipStreamBeginCapture(ctx->stream, hipStreamCaptureModeThreadLocal));
+  int rc = SPX_OK;
+  for (int i = 0; i < chunk && rc == SPX_OK; ++i) rc = enqueue_pivot(ctx, false);
+  hipError_t e = hipStreamEndCapture(ctx->stream, &g);
+  if (rc) {
+    if (g) (void)hipGraphDestroy(g);
+    return rc;
+  }
+  if (e != hipSuccess) {
+    ctx->err = std::string("hipStreamEndCapture: ") + hipGetErrorString(e);
+    return SPX_E_HIP;
+  }
+  e = hipGraphInstantiate(&ctx->gexec, g, nullptr, nullptr, 0);
+  (void)hipGraphDestroy(g);
+  if (e != hipSuccess) {
+    ctx->gexec = nullptr;
+    ctx->err = std::string("hipGraphInstantiate: ") + hipGetErrorString(e);
+    return SPX_E_HIP;
+  }
+  ctx->gchunk = chunk;
+  return SPX_OK;
+}
+
+int map_status(int32_t st) {
+  switch (st) {
+    case ST_OPTIMAL: return SPX_OPTIMAL;
+    case ST_UNBOUNDED: return SPX_UNBOUNDED;
+    case ST_LIMIT: return SPX_ITER_LIMIT;
+    default: return SPX_RUNNING;
+  }
+}
+
+int alloc_common(spx_ctx* ctx, int64_t m_local, int64_t N, int64_t m_global, int64_t row0) {
+  free_buffers(ctx);
+  ctx->m_local = m_local;
+  ctx->m_global = m_global;
+  ctx->row0 = row0;
+  ctx->N = N;
+  ctx->ld = std::max<int64_t>(64, round_up(m_local, 64));
+  choose_geometry(ctx);
+  ctx->hist_cap = 1 << 20;
+  HIPC(hipSetDevice(ctx->device));
+  HIPC(hipMalloc(&ctx->A, sizeof(double) * ctx->ld * N));
+  HIPC(hipMalloc(&ctx->obj, sizeof(double) * N));
+  HIPC(hipMalloc(&ctx->F, sizeof(double) * ctx->ld));
+  HIPC(hipMalloc(&ctx->P, sizeof(double) * N));
+  HIPC(hipMalloc(&ctx->list, sizeof(int) * N));
+  HIPC(hipMalloc(&ctx->basis, sizeof(int64_t) * std::max<int64_t>(1, m_global)));
+  HIPC(hipMalloc(&ctx->hist, sizeof(int64_t) * 2 * ctx->hist_cap));
+  HIPC(hipMalloc(&ctx->enter_part, sizeof(Key) * ctx->nbn));
+  HIPC(hipMalloc(&ctx->ratio_part, sizeof(Key) * ctx->nbr));
+  HIPC(hipMalloc(&ctx->sendkey, sizeof(Key)));
+  HIPC(hipMalloc(&ctx->keys_all, sizeof(Key) * ctx->nranks));
+  HIPC(hipMemsetAsync(ctx->A, 0, sizeof(double) * ctx->ld * N, ctx->stream));
+  HIPC(hipMemsetAsync(ctx->F, 0, sizeof(double) * ctx->ld, ctx->stream));
+  HIPC(hipMemsetAsync(ctx->P, 0, sizeof(double) * N, ctx->stream));
+  std::memset(ctx->h_st, 0, sizeof(State));
+  ctx->h_st->status = ST_RUNNING;
+  ctx->h_st->forced_c = -1;
+  ctx->h_st->forced_r = -1;
+  ctx->h_st->hist_cap = ctx->hist_cap;
+  HIPC(hipMemcpyAsync(ctx->st, ctx->h_st, sizeof(State), hipMemcpyHostToDevice, ctx->stream));
+  return SPX_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+void spx_default_opts(spx_opts* o) {
+  if (!o) return;
+  std::memset(o, 0, sizeof(*o));
+  o->rule = SPX_RULE_DANTZIG;
+  o->skip_zero_cols = 1;
+  o->eps_opt = 1e-9;
+  o->eps_piv = 1e-12;
+  o->max_iters = 0;
+  o->time_limit_s = 0.0;
+  o->n_enter = 0;
+  o->chunk = 32;
+  o->use_graph = 1;
+}
+
+int spx_abi_version(void) { return SPX_ABI_VERSION; }
+
+const char* spx_last_error(const spx_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+int spx_create(spx_ctx** out, int device) {
+  if (!out) return SPX_E_ARG;
+  *out = nullptr;
+  spx_ctx* ctx = new spx_ctx();
+  ctx->device = device;
+  hipError_t e = hipSetDevice(device);
+  if (e == hipSuccess) e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
+  if (e == hipSuccess) e = hipMalloc(&ctx->prm, sizeof(Params));
+  if (e == hipSuccess) e = hipMalloc(&ctx->st, sizeof(State));
+  if (e == hipSuccess) e = hipHostMalloc(&ctx->h_st, sizeof(State), hipHostMallocDefault);
+  if (e != hipSuccess) {
+    ctx->err = std::string("spx_create: ") + hipGetErrorString(e);
+    *out = ctx;  // caller may read the error, then destroy
+    return SPX_E_HIP;
+  }
+  std::memset(ctx->h_st, 0, sizeof(State));
+  *out = ctx;
+  return SPX_OK;
+}
+
+int spx_comm_unique_id(char out_id[128]) {
+  if (!out_id) return SPX_E_ARG;
+  ncclUniqueId id;
+  if (ncclGetUniqueId(&id) != ncclSuccess) return SPX_E_RCCL;
+  static_assert(sizeof(id) == 128, "ncclUniqueId size");
+  std::memcpy(out_id, &id, sizeof(id));
+  return SPX_OK;
+}
+
+int spx_create_sharded(spx_ctx** out, int device, int rank, int nranks, const char id[128]) {
+  int rc = spx_create(out, device);
+  if (rc) return rc;
+  spx_ctx* ctx = *out;
+  CHECK_ARG(nranks >= 1 && rank >= 0 && rank < nranks && id, "bad rank/nranks/id");
+  ctx->rank = rank;
+  ctx->nranks = nranks;
+  ctx->sharded = true;
+  ncclUniqueId uid;
+  std::memcpy(&uid, id, sizeof(uid));
+  NCCLC(ncclCommInitRank(&ctx->comm, nranks, uid, rank));
+  return SPX_OK;
+}
+
+int spx_destroy(spx_ctx* ctx) {
+  if (!ctx) return SPX_OK;
+  (void)hipSetDevice(ctx->device);
+  if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+  free_buffers(ctx);
+  for (auto& e : ctx->ev) {
+    (void)hipEventDestroy(e.first);
+    (void)hipEventDestroy(e.second);
+  }
+  if (ctx->comm) (void)ncclCommDestroy(ctx->comm);
+  dfree(ctx->prm);
+  dfree(ctx->st);
+  if (ctx->h_st) (void)hipHostFree(ctx->h_st);
+  if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+  delete ctx;
+  return SPX_OK;
+}
+
+int spx_load_rows(spx_ctx* ctx, const double* A, int64_t m_local, int64_t cols, int64_t ld,
+                  int layout, const double* obj, const int64_t* basis, int64_t m_global,
+                  int64_t row0) {
+  if (!ctx) return SPX_E_ARG;
+  CHECK_ARG(cols >= 1 && m_local >= 0 && m_global >= m_local && row0 >= 0 &&
+                row0 + m_local <= m_global,
+            "bad dimensions");
+  CHECK_ARG(obj && (m_global == 0 || basis) && (m_local == 0 || A), "null buffer");
+  CHECK_ARG(layout == SPX_ROW_MAJOR || layout == SPX_COL_MAJOR, "bad layout");
+  CHECK_ARG(m_local == 0 || (layout == SPX_ROW_MAJOR ? ld >= cols : ld >= m_local), "bad ld");
+  CHECK_ARG(cols < INT32_MAX, "too many columns");
+  int rc = alloc_common(ctx, m_local, cols, m_global, row0);
+  if (rc) return rc;
+  if (m_local > 0) {
+    if (layout == SPX_COL_MAJOR) {
+      HIPC(hipMemcpy2DAsync(ctx->A, sizeof(double) * ctx->ld, A, sizeof(double) * ld,
+                            sizeof(double) * m_local, cols, hipMemcpyHostToDevice,
+                            ctx->stream));
+    } else {
+      // blocked host transpose into a column-major staging buffer
+      std::vector<double> stage((size_t)ctx->ld * cols, 0.0);
+      const int64_t B = 64;
+      for (int64_t i0 = 0; i0 < m_local; i0 += B)
+        for (int64_t j0 = 0; j0 < cols; j0 += B)
+          for (int64_t i = i0; i < std::min(i0 + B, m_local); ++i)
+            for (int64_t j = j0; j < std::min(j0 + B, cols); ++j)
+              stage[(size_t)j * ctx->ld + i] = A[i * ld + j];
+      HIPC(hipMemcpyAsync(ctx->A, stage.data(), sizeof(double) * stage.size(),
+                          hipMemcpyHostToDevice, ctx->stream));
+      HIPC(hipStreamSynchronize(ctx->stream));
+    }
+  }
+  HIPC(hipMemcpyAsync(ctx->obj, obj, sizeof(double) * cols, hipMemcpyHostToDevice, ctx->stream));
+  if (m_global > 0)
+    HIPC(hipMemcpyAsync(ctx->basis, basis, sizeof(int64_t) * m_global, hipMemcpyHostToDevice,
+                        ctx->stream));
+  HIPC(hipStreamSynchronize(ctx->stream));
+  ctx->loaded = true;
+  return SPX_OK;
+}
+
+int spx_load(spx_ctx* ctx, const double* T, int64_t rows, int64_t cols, int64_t ld, int layout,
+             const int64_t* basis) {
+  if (!ctx) return SPX_E_ARG;
+  CHECK_ARG(T && rows >= 1 && cols >= 1, "bad tableau");
+  CHECK_ARG(!ctx->sharded || ctx->nranks == 1, "use spx_load_rows on a sharded context");
+  const int64_t m = rows - 1;
+  std::vector<double> objrow((size_t)cols);
+  for (int64_t j = 0; j < cols; ++j)
+    objrow[j] = (layout == SPX_ROW_MAJOR) ? T[m * ld + j] : T[j * ld + m];
+  return spx_load_rows(ctx, T, m, cols, ld, layout, objrow.data(), basis, m, 0);
+}
+
+int spx_set_objective(spx_ctx* ctx, const double* obj) {
+  if (!ctx) return SPX_E_ARG;
+  CHECK_ARG(ctx->loaded && obj, "no tableau / null objective");
+  HIPC(hipMemcpyAsync(ctx->obj, obj, sizeof(double) * ctx->N, hipMemcpyHostToDevice,
+                      ctx->stream));
+  HIPC(hipStreamSynchronize(ctx->stream));
+  return SPX_OK;
+}
+
+int spx_get_tableau(spx_ctx* ctx, double* out, int64_t ld, int layout) {
+  if (!ctx) return SPX_E_ARG;
+  CHECK_ARG(ctx->loaded && out, "no tableau / null buffer");
+  CHECK_ARG(layout == SPX_ROW_MAJOR || layout == SPX_COL_MAJOR, "bad layout");
+  const int64_t rows = ctx->m_local + 1, N = ctx->N;
+  CHECK_ARG(layout == SPX_ROW_MAJOR ? ld >= N : ld >= rows, "bad ld");
+  std::vector<double> stage((size_t)ctx->ld * N), o((size_t)N);
+  HIPC(hipMemcpyAsync(stage.data(), ctx->A, sizeof(double) * stage.size(),
+                      hipMemcpyDeviceToHost, ctx->stream));
+  HIPC(hipMemcpyAsync(o.data(), ctx->obj, sizeof(double) * N, hipMemcpyDeviceToHost,
+                      ctx->stream));
+  HIPC(hipStreamSynchronize(ctx->stream));
+  for (int64_t j = 0; j < N; ++j) {
+    for (int64_t i = 0; i < ctx->m_local; ++i) {
+      const double v = stage[(size_t)j * ctx->ld + i];
+      if (layout == SPX_ROW_MAJOR) out[i * ld + j] = v;
+      else out[j * ld + i] = v;
+    }
+    if (layout == SPX_ROW_MAJOR) out[ctx->m_local * ld + j] = o[j];
+    else out[j * ld + ctx->m_local] = o[j];
+  }
+  return SPX_OK;
+}
+
+int spx_get_objective(spx_ctx* ctx, double* out) {
+  if (!ctx) return SPX_E_ARG;
+  CHECK_ARG(ctx->loaded && out, "no tableau / null buffer");
+  HIPC(hipMemcpyAsync(out, ctx->obj, sizeof(double) * ctx->N, hipMemcpyDeviceToHost,
+                      ctx->stream));
+  HIPC(hipStreamSynchronize(ctx->stream));
+  return SPX_OK;
+}
+
+int spx_get_basis(spx_ctx* ctx, int64_t* out) {
+  if (!ctx) return SPX_E_ARG;
+  CHECK_ARG(ctx->loaded && out, "no tableau / null buffer");
+  if (ctx->m_global > 0) {
+    HIPC(hipMemcpyAsync(out, ctx->basis, sizeof(int64_t) * ctx->m_global, hipMemcpyDeviceToHost,
+                        ctx->stream));
+    HIPC(hipStreamSynchronize(ctx->stream));
+  }
+  return SPX_OK;
+}
+
+int spx_get_column(spx_ctx* ctx, int64_t j, double* out) {
+  if (!ctx) return SPX_E_ARG;
+  CHECK_ARG(ctx->loaded && out && j >= 0 && j < ctx->N, "bad column");
+  if (ctx->m_local > 0) {
+    HIPC(hipMemcpyAsync(out, ctx->A + j * ctx->ld, sizeof(double) * ctx->m_local,
+                        hipMemcpyDeviceToHost, ctx->stream));
+    HIPC(hipStreamSynchronize(ctx->stream));
+  }
+  return SPX_OK;
+}
+
+int spx_get_history(spx_ctx* ctx, int64_t* rc_pairs, int64_t cap, int64_t* n) {
+  if (!ctx) return SPX_E_ARG;
+  CHECK_ARG(ctx->loaded && n && (cap == 0 || rc_pairs), "bad history args");
+  int rc = pull_state(ctx);
+  if (rc) return rc;
+  const int64_t have = std::min(ctx->h_st->iters, ctx->hist_cap);
+  *n = ctx->h_st->iters;
+  const int64_t k = std::min(have, cap);
+  if (k > 0) {
+    HIPC(hipMemcpyAsync(rc_pairs, ctx->hist, sizeof(int64_t) * 2 * k, hipMemcpyDeviceToHost,
+                        ctx->stream));
+    HIPC(hipStreamSynchronize(ctx->stream));
+  }
+  return SPX_OK;
+}
+
+int spx_dims(const spx_ctx* ctx, int64_t* m_global, int64_t* m_local, int64_t* cols,
+             int64_t* row0) {
+  if (!ctx) return SPX_E_ARG;
+  if (m_global) *m_global = ctx->m_global;
+  if (m_local) *m_local = ctx->m_local;
+  if (cols) *cols = ctx->N;
+  if (row0) *row0 = ctx->row0;
+  return SPX_OK;
+}
+
+int spx_solve(spx_ctx* ctx, const spx_opts* opts, spx_result* res) {
+  if (!ctx) return SPX_E_ARG;
+  spx_opts d;
+  spx_default_opts(&d);
+  const spx_opts* o = opts ? opts : &d;
+  const auto t0 = std::chrono::steady_clock::now();
+  int rc = begin_call(ctx, o);
+  if (rc) return rc;
+  const int64_t it0 = ctx->h_st->iters;
+  const int chunk = o->chunk > 0 ? o->chunk : 32;
+  bool use_graph = o->use_graph != 0;
+  if (use_graph) {
+    rc = build_graph(ctx, chunk);
+    if (rc) return rc;
+  }
+  int status = SPX_RUNNING;
+  for (;;) {
+    if (use_graph) {
+      HIPC(hipGraphLaunch(ctx->gexec, ctx->stream));
+    } else {
+      for (int i = 0; i < chunk; ++i)
+        if ((rc = enqueue_pivot(ctx, false))) return rc;
+    }
+    if ((rc = pull_state(ctx))) return rc;
+    status = map_status(ctx->h_st->status);
+    if (status != SPX_RUNNING) break;
+    const double el =
+        std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    if (o->time_limit_s > 0 && el >= o->time_limit_s) {
+      status = SPX_ITER_LIMIT;
+      break;
+    }
+  }
+  double z = 0.0;
+  HIPC(hipMemcpyAsync(&z, ctx->obj + (ctx->N - 1), sizeof(double), hipMemcpyDeviceToHost,
+                      ctx->stream));
+  HIPC(hipStreamSynchronize(ctx->stream));
+  if (res) {
+    res->status = status;
+    res->pad = 0;
+    res->iters = ctx->h_st->iters - it0;
+    res->objective = z;
+    res->elapsed_s =
+        std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  }
+  return status;
+}
+
+int spx_pivot(spx_ctx* ctx, const spx_opts* opts, int64_t* r, int64_t* c) {
+  if (!ctx) return SPX_E_ARG;
+  int rc = begin_call(ctx, opts);
+  if (rc) return rc;
+  const int64_t it0 = ctx->h_st->iters;
+  if ((rc = enqueue_pivot(ctx, false))) return rc;
+  if ((rc = pull_state(ctx))) return rc;
+  const int status = map_status(ctx->h_st->status);
+  if (status == SPX_RUNNING && ctx->h_st->iters == it0 + 1) {
+    if (r) *r = ctx->h_st->r;
+    if (c) *c = ctx->h_st->c;
+    return SPX_RUNNING;
+  }
+  if (r) *r = -1;
+  if (c) *c = -1;
+  return status == SPX_RUNNING ? SPX_E_STATE : status;
+}
+
+int spx_pivot_at(spx_ctx* ctx, int64_t r, int64_t c) {
+  if (!ctx) return SPX_E_ARG;
+  CHECK_ARG(ctx->loaded && r >= 0 && r < ctx->m_global && c >= 0 && c < ctx->N - 1,
+            "pivot position out of range");
+  int rc = begin_call(ctx, nullptr);
+  if (rc) return rc;
+  if ((rc = set_state_fields(ctx, ST_RUNNING, c, r))) return rc;
+  if ((rc = enqueue_pivot(ctx, false))) return rc;
+  // pull the post-pivot state before writing the forced fields back
+  if ((rc = pull_state(ctx))) return rc;
+  const int32_t st_after = ctx->h_st->status;
+  if ((rc = set_state_fields(ctx, st_after, -1, -1))) return rc;
+  if ((rc = pull_state(ctx))) return rc;
+  return st_after == ST_RUNNING ? SPX_OK : SPX_E_STATE;
+}
+
+int spx_run_pivots(spx_ctx* ctx, const spx_opts* opts, int64_t npivots, int time_elim) {
+  if (!ctx) return SPX_E_ARG;
+  CHECK_ARG(npivots >= 0, "npivots < 0");
+  spx_opts d;
+  spx_default_opts(&d);
+  const spx_opts* o = opts ? opts : &d;
+  int rc = begin_call(ctx, o);
+  if (rc) return rc;
+  if (!time_elim && o->use_graph) {
+    const int chunk = o->chunk > 0 ? o->chunk : 32;
+    if ((rc = build_graph(ctx, chunk))) return rc;
+    int64_t left = npivots;
+    for (; left >= chunk; left -= chunk) HIPC(hipGraphLaunch(ctx->gexec, ctx->stream));
+    for (; left > 0; --left)
+      if ((rc = enqueue_pivot(ctx, false))) return rc;
+  } else {
+    for (int64_t i = 0; i < npivots; ++i)
+      if ((rc = enqueue_pivot(ctx, time_elim != 0))) return rc;
+  }
+  return SPX_OK;
+}
+
+int spx_sync(spx_ctx* ctx) {
+  if (!ctx) return SPX_E_ARG;
+  HIPC(hipStreamSynchronize(ctx->stream));
+  return SPX_OK;
+}
+
+int spx_state(spx_ctx* ctx, int32_t* status, int64_t* iters, double* objective) {
+  if (!ctx) return SPX_E_ARG;
+  CHECK_ARG(ctx->loaded, "no tableau loaded");
+  int rc = pull_state(ctx);
+  if (rc) return rc;
+  if (status) *status = map_status(ctx->h_st->status);
+  if (iters) *iters = ctx->h_st->iters;
+  if (objective) {
+    HIPC(hipMemcpyAsync(objective, ctx->obj + (ctx->N - 1), sizeof(double),
+                        hipMemcpyDeviceToHost, ctx->stream));
+    HIPC(hipStreamSynchronize(ctx->stream));
+  }
+  return SPX_OK;
+}
+
+int spx_elim_timing(spx_ctx* ctx, double* total_ms, int64_t* count, int64_t* touched_cols,
+                    int reset) {
+  if (!ctx) return SPX_E_ARG;
+  HIPC(hipStreamSynchronize(ctx->stream));
+  double tot = 0.0;
+  for (size_t i = 0; i < ctx->ev_used; ++i) {
+    float ms = 0.f;
+    HIPC(hipEventElapsedTime(&ms, ctx->ev[i].first, ctx->ev[i].second));
+    tot += ms;
+  }
+  int rc = pull_state(ctx);
+  if (rc) return rc;
+  if (total_ms) *total_ms = tot;
+  if (count) *count = (int64_t)ctx->ev_used;
+  if (touched_cols) *touched_cols = ctx->h_st->touched_total - ctx->touched_at_reset;
+  if (reset) {
+    ctx->ev_used = 0;
+    ctx->touched_at_reset = ctx->h_st->touched_total;
+  }
+  return SPX_OK;
+}
+
+// Tuning knob (not part of the stable ABI): non-temporal elimination stream.
+int spx_set_elim_nt(spx_ctx* ctx, int nt) {
+  if (!ctx) return SPX_E_ARG;
+  if ((nt != 0) != (ctx->elim_nt != 0)) {
+    ctx->elim_nt = nt;
+    if (ctx->gexec) (void)hipGraphExecDestroy(ctx->gexec);
+    ctx->gexec = nullptr;
+    ctx->gchunk = 0;
+  }
+  return SPX_OK;
+}
+
+}  // extern "C"

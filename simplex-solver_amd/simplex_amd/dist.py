@@ -1,0 +1,73 @@
+"""Row-sharded tableau across GPUs: one process per GPU, RCCL over xGMI.
+
+Partitioning: constraint rows 0..m-1 are split into contiguous
+blocks, one per rank; the objective row and the basis are replicated.  Every
+rank chooses the entering column locally (identical objective rows give
+identical choices, no collective).  Per pivot libspx issues two RCCL calls on
+the context's stream, both captured in the pivot-chunk hipGraph:
+  1. all-gather of each rank's best (ratio, tie, row) key (32 B per rank) —
+     every rank reduces the gathered keys identically (the leaving-row
+     "allreduce-min", which RCCL has no MINLOC op for);
+  2. all-reduce(sum) of the normalised pivot row, non-owners contributing
+     zeros — the owner's broadcast without a host-known root.
+Results are bit-identical to one GPU (the update is elementwise; the sum has
+exactly one nonzero term per element).
+
+torch.distributed is used only to ship the 128-byte RCCL unique id from rank 0
+to the others (any backend: gloo on CPU, nccl on GPU).
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+from . import _lib as L
+from .engine import DeviceTableau
+
+
+def row_partition(m: int, world: int, rank: int) -> tuple:
+    """Contiguous near-equal block [row0, row1) of rank `rank`."""
+    if world < 1 or not 0 <= rank < world:
+        raise ValueError("bad world/rank")
+    base, extra = divmod(m, world)
+    row0 = rank * base + min(rank, extra)
+    return row0, row0 + base + (1 if rank < extra else 0)
+
+
+def make_unique_id() -> bytes:
+    buf = ctypes.create_string_buffer(128)
+    rc = L.lib().spx_comm_unique_id(buf)
+    if rc != 0:
+        raise RuntimeError(f"spx_comm_unique_id failed ({rc})")
+    return buf.raw
+
+
+def exchange_unique_id(make_id=make_unique_id, group=None) -> bytes:
+    """Rank 0 creates the id, every rank returns it (torch.distributed)."""
+    import torch.distributed as dist
+    obj = [make_id() if dist.get_rank(group) == 0 else None]
+    dist.broadcast_object_list(obj, src=0, group=group)
+    uid = obj[0]
+    if not isinstance(uid, (bytes, bytearray)) or len(uid) != 128:
+        raise RuntimeError("bad RCCL unique id received")
+    return bytes(uid)
+
+
+class ShardedTableau(DeviceTableau):
+    """This rank's row block of a tableau sharded over `world` GPUs."""
+
+    def __init__(self, device: int, rank: int, world: int, uid: bytes):
+        super().__init__(device, _sharded=(rank, world, uid))
+        self.rank, self.world = rank, world
+
+    @classmethod
+    def from_env(cls, device: int | None = None, group=None) -> "ShardedTableau":
+        import torch.distributed as dist
+        rank, world = dist.get_rank(group), dist.get_world_size(group)
+        uid = exchange_unique_id(group=group)
+        return cls(rank if device is None else device, rank, world, uid)
+
+    def load_shard(self, T_rows: np.ndarray, obj: np.ndarray, basis: np.ndarray, m_global: int,
+                   row0: int) -> "ShardedTableau":
+        return self.load_rows(T_rows, obj, basis, m_global, row0)

@@ -1,0 +1,253 @@
+"""Device-resident simplex tableau: the Python face of libspx.so.
+
+``DeviceTableau`` owns one spx context (one HIP stream + the tableau in HBM).
+It is what ``simplex_amd.simple_simplex.optimize_json_format`` (the drop-in
+for the reference's ``simple_simplex`` pivot engine, called at
+app/controllers/solver_controller.py:318) pivots on.
+
+Tableau convention: ``T`` has m+1 rows, objective row LAST in
+the "z_j - c_j" form of a MAX problem, right-hand side in the last column;
+``basis[i]`` is the variable basic in row i.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import _lib as L
+
+RULES = {"dantzig": L.SPX_RULE_DANTZIG, "bland": L.SPX_RULE_BLAND}
+STATUS_NAMES = {L.SPX_OPTIMAL: "optimal", L.SPX_ITER_LIMIT: "iteration_limit",
+                L.SPX_INFEASIBLE: "infeasible", L.SPX_UNBOUNDED: "unbounded",
+                L.SPX_RUNNING: "running"}
+
+
+class SpxError(RuntimeError):
+    """A libspx call failed (HIP / RCCL / argument error)."""
+
+
+@dataclass
+class SolveResult:
+    status: int          # scipy OptimizeResult.status numbering (0,1,2,3)
+    iters: int
+    objective: float     # objective-row RHS (MAX form)
+    elapsed_s: float
+
+    @property
+    def status_name(self) -> str:
+        return STATUS_NAMES.get(self.status, str(self.status))
+
+
+def _dptr(a: np.ndarray):
+    return a.ctypes.data_as(ctypes.POINTER(ctypes.c_double))
+
+
+def _lptr(a: np.ndarray):
+    return a.ctypes.data_as(ctypes.POINTER(ctypes.c_int64))
+
+
+def make_opts(rule="dantzig", eps_opt=1e-9, eps_piv=1e-12, max_iters=0, time_limit=0.0,
+              n_enter=0, chunk=32, use_graph=True, skip_zero_cols=True) -> L.SpxOpts:
+    if isinstance(rule, str):
+        if rule.lower() not in RULES:
+            raise ValueError(f"unknown pivot rule {rule!r}; expected one of {sorted(RULES)}")
+        rule = RULES[rule.lower()]
+    o = L.default_opts()
+    o.rule = int(rule)
+    o.eps_opt = float(eps_opt)
+    o.eps_piv = float(eps_piv)
+    o.max_iters = int(max_iters or 0)
+    o.time_limit_s = float(time_limit or 0.0)
+    o.n_enter = int(n_enter or 0)
+    o.chunk = int(chunk)
+    o.use_graph = 1 if use_graph else 0
+    o.skip_zero_cols = 1 if skip_zero_cols else 0
+    return o
+
+
+class DeviceTableau:
+    """A tableau resident on one GPU (or one row shard of it, see dist.py)."""
+
+    def __init__(self, device: int = 0, *, _sharded=None):
+        self._lib = L.lib()
+        self._ctx = ctypes.c_void_p()
+        if _sharded is None:
+            rc = self._lib.spx_create(ctypes.byref(self._ctx), int(device))
+        else:
+            rank, nranks, uid = _sharded
+            rc = self._lib.spx_create_sharded(ctypes.byref(self._ctx), int(device), int(rank),
+                                              int(nranks), uid)
+        if rc != 0:
+            msg = self._err()
+            self.close()
+            raise SpxError(f"spx_create failed ({rc}): {msg}")
+        self.device = device
+        self.m = self.m_local = self.N = self.row0 = 0
+
+    # -- plumbing -----------------------------------------------------------
+    def _err(self) -> str:
+        if not self._ctx:
+            return "no context"
+        s = self._lib.spx_last_error(self._ctx)
+        return s.decode() if s else ""
+
+    def _check(self, rc: int, what: str) -> int:
+        if rc < 0:
+            raise SpxError(f"{what} failed ({rc}): {self._err()}")
+        return rc
+
+    def close(self) -> None:
+        if getattr(self, "_ctx", None):
+            self._lib.spx_destroy(self._ctx)
+            self._ctx = ctypes.c_void_p()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):  # pragma: no cover - best effort
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _refresh_dims(self):
+        mg, ml, n, r0 = (ctypes.c_int64() for _ in range(4))
+        self._lib.spx_dims(self._ctx, ctypes.byref(mg), ctypes.byref(ml), ctypes.byref(n),
+                           ctypes.byref(r0))
+        self.m, self.m_local, self.N, self.row0 = mg.value, ml.value, n.value, r0.value
+
+    # -- data in ------------------------------------------------------------
+    def load(self, T, basis) -> "DeviceTableau":
+        """Load a full (m+1) x N tableau (objective row last) and its basis."""
+        T = np.asarray(T, dtype=np.float64)
+        if T.ndim != 2 or T.shape[0] < 1 or T.shape[1] < 1:
+            raise ValueError("tableau must be a non-empty 2-D array")
+        m = T.shape[0] - 1
+        basis = np.ascontiguousarray(np.asarray(basis, dtype=np.int64).reshape(-1))
+        if basis.shape[0] != m:
+            raise ValueError(f"basis has {basis.shape[0]} entries, tableau has {m} rows")
+        if np.isfortran(T) and not T.flags.c_contiguous:
+            layout, ld = L.SPX_COL_MAJOR, T.shape[0]
+        else:
+            T = np.ascontiguousarray(T)
+            layout, ld = L.SPX_ROW_MAJOR, T.shape[1]
+        self._check(self._lib.spx_load(self._ctx, _dptr(T), T.shape[0], T.shape[1], ld, layout,
+                                       _lptr(basis)), "spx_load")
+        self._refresh_dims()
+        return self
+
+    def load_rows(self, A, obj, basis, m_global: int, row0: int) -> "DeviceTableau":
+        """Load constraint rows [row0, row0 + A.shape[0]) plus the objective row."""
+        A = np.asarray(A, dtype=np.float64)
+        if A.ndim != 2:
+            raise ValueError("A must be 2-D")
+        obj = np.ascontiguousarray(np.asarray(obj, dtype=np.float64).reshape(-1))
+        basis = np.ascontiguousarray(np.asarray(basis, dtype=np.int64).reshape(-1))
+        if obj.shape[0] != A.shape[1]:
+            raise ValueError("objective row length != number of columns")
+        if basis.shape[0] != m_global:
+            raise ValueError("basis length != m_global")
+        if np.isfortran(A) and not A.flags.c_contiguous:
+            layout, ld = L.SPX_COL_MAJOR, max(1, A.shape[0])
+        else:
+            A = np.ascontiguousarray(A)
+            layout, ld = L.SPX_ROW_MAJOR, A.shape[1]
+        self._check(self._lib.spx_load_rows(self._ctx, _dptr(A), A.shape[0], A.shape[1], ld,
+                                            layout, _dptr(obj), _lptr(basis), int(m_global),
+                                            int(row0)), "spx_load_rows")
+        self._refresh_dims()
+        return self
+
+    def set_objective(self, obj) -> None:
+        obj = np.ascontiguousarray(np.asarray(obj, dtype=np.float64).reshape(-1))
+        if obj.shape[0] != self.N:
+            raise ValueError("objective row length != number of columns")
+        self._check(self._lib.spx_set_objective(self._ctx, _dptr(obj)), "spx_set_objective")
+
+    # -- data out -----------------------------------------------------------
+    def tableau(self) -> np.ndarray:
+        out = np.empty((self.m_local + 1, self.N), dtype=np.float64)
+        self._check(self._lib.spx_get_tableau(self._ctx, _dptr(out), self.N, L.SPX_ROW_MAJOR),
+                    "spx_get_tableau")
+        return out
+
+    def objective_row(self) -> np.ndarray:
+        out = np.empty(self.N, dtype=np.float64)
+        self._check(self._lib.spx_get_objective(self._ctx, _dptr(out)), "spx_get_objective")
+        return out
+
+    def basis(self) -> np.ndarray:
+        out = np.empty(max(self.m, 0), dtype=np.int64)
+        if self.m:
+            self._check(self._lib.spx_get_basis(self._ctx, _lptr(out)), "spx_get_basis")
+        return out
+
+    def column(self, j: int) -> np.ndarray:
+        out = np.empty(self.m_local, dtype=np.float64)
+        self._check(self._lib.spx_get_column(self._ctx, int(j), _dptr(out)), "spx_get_column")
+        return out
+
+    def history(self) -> np.ndarray:
+        """(k, 2) int64 array of (row, col) pivots since load."""
+        n = ctypes.c_int64()
+        self._check(self._lib.spx_get_history(self._ctx, None, 0, ctypes.byref(n)),
+                    "spx_get_history")
+        k = n.value
+        out = np.empty((k, 2), dtype=np.int64)
+        if k:
+            self._check(self._lib.spx_get_history(self._ctx, _lptr(out), k, ctypes.byref(n)),
+                        "spx_get_history")
+        return out
+
+    # -- pivoting -----------------------------------------------------------
+    def solve(self, **kw) -> SolveResult:
+        o = make_opts(**kw)
+        res = L.SpxResult()
+        rc = self._lib.spx_solve(self._ctx, ctypes.byref(o), ctypes.byref(res))
+        self._check(rc, "spx_solve")
+        return SolveResult(int(res.status), int(res.iters), float(res.objective),
+                           float(res.elapsed_s))
+
+    def pivot(self, **kw):
+        """One rule-chosen pivot: returns (r, c), or the terminal status
+        (L.SPX_OPTIMAL / L.SPX_UNBOUNDED) when no pivot is possible."""
+        o = make_opts(**kw)
+        r, c = ctypes.c_int64(), ctypes.c_int64()
+        rc = self._check(self._lib.spx_pivot(self._ctx, ctypes.byref(o), ctypes.byref(r),
+                                             ctypes.byref(c)), "spx_pivot")
+        if rc == L.SPX_RUNNING:
+            return int(r.value), int(c.value)
+        return rc
+
+    def pivot_at(self, r: int, c: int) -> None:
+        self._check(self._lib.spx_pivot_at(self._ctx, int(r), int(c)), "spx_pivot_at")
+
+    def run_pivots(self, npivots: int, time_elim: bool = False, **kw) -> None:
+        o = make_opts(**kw)
+        self._check(self._lib.spx_run_pivots(self._ctx, ctypes.byref(o), int(npivots),
+                                             1 if time_elim else 0), "spx_run_pivots")
+
+    def sync(self) -> None:
+        self._check(self._lib.spx_sync(self._ctx), "spx_sync")
+
+    def state(self):
+        st, it, z = ctypes.c_int32(), ctypes.c_int64(), ctypes.c_double()
+        self._check(self._lib.spx_state(self._ctx, ctypes.byref(st), ctypes.byref(it),
+                                        ctypes.byref(z)), "spx_state")
+        return int(st.value), int(it.value), float(z.value)
+
+    def elim_timing(self, reset: bool = True):
+        """(total_ms, launches, touched_columns) of event-timed eliminations."""
+        ms, cnt, cols = ctypes.c_double(), ctypes.c_int64(), ctypes.c_int64()
+        self._check(self._lib.spx_elim_timing(self._ctx, ctypes.byref(ms), ctypes.byref(cnt),
+                                              ctypes.byref(cols), 1 if reset else 0),
+                    "spx_elim_timing")
+        return float(ms.value), int(cnt.value), int(cols.value)
+
+    def set_elim_nt(self, nt: bool) -> None:
+        self._check(self._lib.spx_set_elim_nt(self._ctx, 1 if nt else 0), "spx_set_elim_nt")

@@ -1,0 +1,316 @@
+"""Parity of the HIP pivot engine (through the C-ABI) with the CPU oracle.
+
+Bar: bit-exact tableaux, pivot sequences and bases (np.array_equal, which
+treats -0.0 == +0.0); objectives additionally within 1e-9 relative of HiGHS.
+"""
+import hashlib
+import importlib.util
+import json
+import os
+import threading
+
+import numpy as np
+import pytest
+
+from oracle import simplex_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+TEXTBOOK = json.load(open(os.path.join(HERE, "textbook.json")))
+DENSE = json.load(open(os.path.join(HERE, "dense_lp.json")))
+
+
+def _mg():
+    spec = importlib.util.spec_from_file_location("make_golden",
+                                                  os.path.join(HERE, "make_golden.py"))
+    mg = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mg)
+    return mg
+
+
+@pytest.fixture(scope="module")
+def eng_cls():
+    from simplex_amd.engine import DeviceTableau
+    return DeviceTableau
+
+
+def _rows(e):
+    return [(a, op, b) for a, op, b in e["rows"]]
+
+
+# ----------------------------------------------------------- single pivots
+def test_single_pivot_vectors_bit_exact(eng_cls):
+    """spx_pivot_at on the golden single-pivot inputs (tests/golden/pivots*)."""
+    mg = _mg()
+    digests = json.load(open(os.path.join(HERE, "pivots_sha256.json")))
+    for k in range(len(mg.PIVOT_SHAPES)):
+        T, r, c = mg.pivot_case(k)
+        if T.shape[0] < 2:
+            continue
+        basis = np.arange(T.shape[0] - 1, dtype=np.int64)
+        with eng_cls(0) as e:
+            e.load(T, basis)
+            e.pivot_at(r, c)
+            out = e.tableau()
+        ref = T.copy()
+        O.pivot(ref, r, c, skip_zero=True)
+        assert np.array_equal(out, ref), f"case {k}"
+        assert hashlib.sha256(ref.tobytes()).hexdigest() == digests[f"case{k}_after_skip"]
+        # bit-level: the only allowed difference is none at all here
+        assert out.tobytes() == ref.tobytes(), f"case {k}: not bitwise identical"
+
+
+@pytest.mark.parametrize("shape", [(2, 3), (17, 40), (300, 700), (1025, 2051), (2049, 4097)])
+@pytest.mark.parametrize("skip", [True, False], ids=["skip", "dense"])
+def test_rule_pivots_bit_exact_random(eng_cls, shape, skip):
+    """Rule-chosen pivots on random feasible tableaux: sequence + bits."""
+    rows, cols = shape
+    rng = np.random.default_rng(rows * 7 + cols)
+    m = rows - 1
+    n = cols - 1 - m
+    if n < 1:
+        n = 1
+    A = rng.uniform(0.05, 1.0, size=(m, n))
+    A[rng.random(A.shape) < 0.1] = 0.0
+    T = np.zeros((m + 1, n + m + 1))
+    T[:m, :n] = A
+    T[np.arange(m), n + np.arange(m)] = 1.0
+    T[:m, -1] = rng.uniform(1, 2, size=m) * n
+    T[m, :n] = -rng.uniform(0.1, 1, size=n)
+    basis = np.arange(n, n + m, dtype=np.int64)
+    ref, rb = T.copy(), basis.copy()
+    st, hist = O.solve_tableau(ref, rb, max_iters=12, skip_zero=skip)
+    with eng_cls(0) as e:
+        e.load(T, basis)
+        res = e.solve(max_iters=12, skip_zero_cols=skip)
+        assert [tuple(h) for h in e.history().tolist()] == hist
+        assert np.array_equal(e.tableau(), ref)
+        assert np.array_equal(e.basis(), rb)
+        assert res.status == st
+
+
+# ----------------------------------------------------------- textbook LPs
+@pytest.mark.parametrize("case", TEXTBOOK, ids=[e["name"] for e in TEXTBOOK])
+@pytest.mark.parametrize("rule", ["dantzig", "bland"])
+def test_textbook_through_simple_simplex(case, rule):
+    from simplex_amd import simple_simplex as ss
+    n = len(case["c"])
+    t = ss.create_tableau(number_of_variables=n, number_of_constraints=len(case["rows"]))
+    for a, op, b in case["rows"]:
+        code = {"<=": "L", ">=": "G", "=": "E"}[op]
+        t_str = ",".join(str(x) for x in a) + f",{code},{b}"
+        ss.add_constraint(t, t_str)
+    ss.add_objective(t, ",".join(str(x) for x in case["c"]) + (",1" if case["maximize"] else ",0"))
+    out = ss.optimize_json_format(t, maximize=case["maximize"], rule=rule, max_iters=200)
+    g = case[rule]
+    assert out["status_code"] == g["status"]
+    steps = out["pivotSteps"]
+    got = [[s["phase"], s["pivotRowIndex"], s["pivotColIndex"]] for s in steps
+           if s["pivotRowIndex"] is not None]
+    assert got == g["pivots"]
+    assert out["basis"] == g["basis"]
+    assert np.array_equal(np.array(steps[-1]["tableau"]), np.array(g["final_tableau"]))
+    if g["status"] == 0:
+        assert out["objective"] == g["objective"]
+        hz = case["highs"]["objective"]
+        assert abs(out["objective"] - hz) <= 1e-9 * max(1, abs(hz))
+    # every recorded snapshot equals the oracle replayed to that step
+    r = O.standard_form(case["c"], _rows(case), case["maximize"])
+    assert np.array_equal(np.array(steps[0]["tableau"]), r["T"])
+
+
+# ----------------------------------------------------------- generated LPs
+@pytest.mark.parametrize("e", DENSE, ids=lambda e: f"{e['kind']}{e['m']}x{e['n']}")
+def test_generated_lp_full_solve(eng_cls, e):
+    from simplex_amd import synth
+    T, basis = synth.full_tableau(e["kind"], e["m"], e["n"], e["seed"])
+    rule = e.get("rule", "dantzig")
+    with eng_cls(0) as eng:
+        eng.load(T, basis)
+        res = eng.solve(rule=rule)
+        hist = eng.history()
+        assert res.status == 0
+        assert len(hist) == e["oracle_pivots"]
+        assert hist[:32].tolist() == e["oracle_first_pivots"]
+        assert res.objective == e["oracle_objective"]
+        hz = e["highs_objective"]
+        assert abs(res.objective - hz) <= 1e-9 * max(1.0, abs(hz))
+        if e["m"] <= 256:
+            ref, rb = T.copy(), basis.copy()
+            O.solve_tableau(ref, rb, rule=rule, max_iters=200000)
+            assert np.array_equal(eng.tableau(), ref)
+            assert np.array_equal(eng.basis(), rb)
+
+
+def test_config2_full_history_matches_oracle(eng_cls):
+    """1024x2048 random feasible LP (BASELINE config 2): every pivot index."""
+    from simplex_amd import synth
+    e = [d for d in DENSE if d["m"] == 1024][0]
+    T, basis = synth.full_tableau("dense", 1024, 2048, e["seed"])
+    ref, rb = T.copy(), basis.copy()
+    st, hist = O.solve_tableau(ref, rb)
+    with eng_cls(0) as eng:
+        eng.load(T, basis)
+        res = eng.solve()
+        assert [tuple(h) for h in eng.history().tolist()] == hist
+        assert np.array_equal(eng.basis(), rb)
+        assert np.array_equal(eng.tableau(), ref)
+        assert res.objective == ref[-1, -1]
+
+
+def test_degenerate_bland_every_pivot(eng_cls):
+    from simplex_amd import synth
+    T, basis = synth.full_tableau("degenerate", 96, 96, 9)
+    ref, rb = T.copy(), basis.copy()
+    seen = []
+    st, hist = O.solve_tableau(ref, rb, rule="bland", max_iters=100000,
+                               on_pivot=lambda r, c, _T: seen.append(rb.copy()))
+    assert st == 0
+    with eng_cls(0) as eng:
+        eng.load(T, basis)
+        # step through, checking the basis after every pivot
+        for k in range(min(60, len(hist))):
+            out = eng.pivot(rule="bland")
+            assert out == hist[k]
+            assert np.array_equal(eng.basis(), seen[k])
+        res = eng.solve(rule="bland")
+        assert res.status == 0
+        assert [tuple(h) for h in eng.history().tolist()] == hist
+        assert np.array_equal(eng.tableau(), ref)
+
+
+# ----------------------------------------------------------- modes, edges
+def test_graph_and_direct_and_chunks_agree(eng_cls):
+    from simplex_amd import synth
+    T, basis = synth.full_tableau("dense", 200, 300, 11)
+    outs = []
+    for kw in (dict(use_graph=True, chunk=32), dict(use_graph=False, chunk=8),
+               dict(use_graph=True, chunk=1), dict(use_graph=True, chunk=7)):
+        with eng_cls(0) as eng:
+            eng.load(T, basis)
+            res = eng.solve(**kw)
+            outs.append((res.status, res.iters, eng.history().tolist(), eng.tableau()))
+    for o in outs[1:]:
+        assert o[0] == outs[0][0] and o[1] == outs[0][1] and o[2] == outs[0][2]
+        assert np.array_equal(o[3], outs[0][3])
+
+
+def test_iteration_limit_and_resume(eng_cls):
+    from simplex_amd import synth
+    T, basis = synth.full_tableau("dense", 64, 96, 7)
+    with eng_cls(0) as a, eng_cls(0) as b:
+        a.load(T, basis)
+        b.load(T, basis)
+        r1 = a.solve(max_iters=5)
+        assert r1.status == 1 and r1.iters == 5
+        r2 = a.solve()
+        rb = b.solve()
+        assert r2.status == rb.status == 0 and r1.iters + r2.iters == rb.iters
+        assert a.history().tolist() == b.history().tolist()
+        assert np.array_equal(a.tableau(), b.tableau())
+
+
+def test_beale_cycles_under_dantzig_and_bland_terminates(eng_cls):
+    from simplex_amd import lp
+    c = [0.75, -20, 0.5, -6]
+    rows = [([0.25, -8, -1, 9], "<=", 0), ([0.5, -12, -0.5, 3], "<=", 0),
+            ([0, 0, 1, 0], "<=", 1)]
+    sf = lp.build_standard_form(c, rows, True)
+    with eng_cls(0) as e:
+        e.load(sf.T, sf.basis)
+        res = e.solve(max_iters=60)
+        h = e.history().tolist()
+        assert res.status == 1 and h[:6] == h[6:12]
+    res = lp.solve_lp(c, rows, True, rule="bland")
+    assert res.status == 0 and abs(res.objective - 1.25) < 1e-12 and res.iters == 6
+
+
+def test_edges(eng_cls):
+    # no constraints: any improving column is unbounded
+    with eng_cls(0) as e:
+        e.load(np.array([[-1.0, -2.0, 0.0]]), np.zeros(0, dtype=np.int64))
+        assert e.solve().status == 3
+    # already optimal
+    with eng_cls(0) as e:
+        e.load(np.array([[1.0, 1.0, 0.0, 4.0], [1.0, 0.0, 0.0, 0.0]]), np.array([2]))
+        r = e.solve()
+        assert r.status == 0 and r.iters == 0
+    # unbounded column
+    with eng_cls(0) as e:
+        e.load(np.array([[-1.0, 1.0, 1.0, 1.0], [-1.0, -1.0, 0.0, 0.0]]), np.array([2]))
+        assert e.solve().status == 3
+
+
+def test_concurrent_contexts_from_threads(eng_cls):
+    """/solve is entered from many threads (reference test_performance_load.py:80-83)."""
+    from simplex_amd import synth
+    cases = [(40 + 9 * k, 60 + 7 * k, k) for k in range(6)]
+    errors, results = [], {}
+
+    def work(m, n, s):
+        try:
+            T, basis = synth.full_tableau("dense", m, n, s)
+            with eng_cls(0) as e:
+                e.load(T, basis)
+                results[s] = (e.solve().objective, e.history().tolist())
+        except Exception as ex:  # pragma: no cover
+            errors.append(ex)
+
+    th = [threading.Thread(target=work, args=c) for c in cases]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert not errors
+    for m, n, s in cases:
+        T, basis = synth.full_tableau("dense", m, n, s)
+        st, hist = O.solve_tableau(T, basis)
+        assert results[s][0] == T[-1, -1] and [tuple(h) for h in results[s][1]] == hist
+
+
+def test_sharded_single_rank_matches_plain(eng_cls):
+    """RCCL communicator of one rank: exercises the sharded kernels
+    (select / all-gather / PROW / all-reduce / FINISH) end to end."""
+    from simplex_amd import dist, synth
+    T, basis = synth.full_tableau("dense", 200, 300, 11)
+    ref, rb = T.copy(), basis.copy()
+    st, hist = O.solve_tableau(ref, rb)
+    uid = dist.make_unique_id()
+    with dist.ShardedTableau(0, 0, 1, uid) as s:
+        s.load_shard(T[:-1], T[-1], basis, 200, 0)
+        res = s.solve()
+        assert res.status == 0
+        assert [tuple(h) for h in s.history().tolist()] == hist
+        assert np.array_equal(s.tableau(), ref)
+
+
+# ----------------------------------------------------------- full size
+def test_config3_size_first_pivots_bit_exact(eng_cls):
+    """8192 x 16385 tableau (BASELINE config 3): first pivots vs oracle, then
+    size-independent invariants over further pivots."""
+    from simplex_amd import synth
+    m = n = 8192
+    Tf, obj, basis = synth.tableau_rows("dense", m, n, 20251205, order="F")
+    with eng_cls(0) as e:
+        e.load_rows(Tf, obj, basis, m, 0)
+        T = np.vstack([np.ascontiguousarray(Tf), obj[None, :]])
+        del Tf
+        rb = basis.copy()
+        st, hist = O.solve_tableau(T, rb, max_iters=3)
+        res = e.solve(max_iters=3)
+        assert [tuple(h) for h in e.history().tolist()] == hist
+        assert np.array_equal(e.tableau(), T)
+        del T
+        z_prev = e.objective_row()[-1]
+        res = e.solve(max_iters=40)
+        assert res.status == 1 and res.iters == 40
+        b = e.basis()
+        assert len(set(b.tolist())) == m
+        objrow = e.objective_row()
+        assert objrow[-1] >= z_prev  # Dantzig from a feasible basis never decreases Z
+        assert np.all(objrow[b] == 0.0)
+        for k in np.random.default_rng(0).choice(m, 16, replace=False):
+            col = e.column(int(b[k]))
+            assert col[k] == 1.0 and np.count_nonzero(col) == 1  # basic columns = e_k
+        assert e.column(m + n).min() >= -1e-9  # RHS stays feasible
