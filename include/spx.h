@@ -101,6 +101,12 @@ int spx_comm_unique_id(char out_id[128]);
 /* Like spx_create, but joins a communicator of nranks contexts; rank r will
  * own a contiguous block of constraint rows (given at load time). */
 int spx_create_sharded(spx_ctx** out, int device, int rank, int nranks, const char id[128]);
+/* Same as spx_create_sharded, but the ranks are contexts of ONE process (one
+ * host thread per rank, any devices, up to 16 ranks) joined by the 128-byte
+ * group id, exchanging through device copies instead of RCCL.  Used to test
+ * the sharded path on a single GPU; not capturable in a hipGraph. */
+int spx_create_sharded_local(spx_ctx** out, int device, int rank, int nranks,
+                             const char id[128]);
 
 /* ---- data in / out ------------------------------------------------------- */
 /* Load a full tableau of `rows` = m+1 rows (objective row LAST) and `cols` = N

@@ -18,8 +18,10 @@
 
 #include <algorithm>
 #include <chrono>
+#include <condition_variable>
 #include <cstdio>
 #include <cstring>
+#include <map>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -28,6 +30,42 @@
 #include "spx_kernels.hpp"
 
 using namespace spx;
+
+// In-process communicator for "virtual ranks": nranks contexts on one GPU,
+// driven by nranks host threads.  Same per-pivot exchange as RCCL (all-gather
+// of the leaving-row keys, sum of the pivot-row buffers), implemented with
+// stream events + a host barrier, so every sharded kernel path can be tested
+// with nranks > 1 on a single-GPU machine.  Not capturable in a hipGraph.
+struct LoopGroup {
+  int n = 0;
+  int refs = 0;
+  std::string key;
+  std::mutex mu;
+  std::condition_variable cv;
+  int arrived = 0;
+  uint64_t gen = 0;
+  bool broken = false;
+  std::vector<spx_ctx*> members;
+  // returns false on timeout (a peer died): the group is then broken for good
+  bool barrier() {
+    std::unique_lock<std::mutex> lk(mu);
+    if (broken) return false;
+    const uint64_t g = gen;
+    if (++arrived == n) {
+      arrived = 0;
+      ++gen;
+      cv.notify_all();
+      return true;
+    }
+    if (!cv.wait_for(lk, std::chrono::seconds(120), [&] { return gen != g || broken; }) ||
+        broken) {
+      broken = true;
+      cv.notify_all();
+      return false;
+    }
+    return true;
+  }
+};
 
 struct spx_ctx {
   int device = 0;
@@ -38,6 +76,9 @@ struct spx_ctx {
   int rank = 0, nranks = 1;
   bool sharded = false;
   ncclComm_t comm = nullptr;
+  LoopGroup* loop = nullptr;   // in-process virtual ranks instead of RCCL
+  hipEvent_t ev_ready = nullptr, ev_done = nullptr;
+  double* Ptmp = nullptr;      // loop all-reduce output
 
   // dims
   int64_t m_global = 0, m_local = 0, row0 = 0, N = 0, ld = 0;
@@ -123,6 +164,7 @@ int free_buffers(spx_ctx* ctx) {
   dfree(ctx->ratio_part);
   dfree(ctx->sendkey);
   dfree(ctx->keys_all);
+  dfree(ctx->Ptmp);
   ctx->loaded = false;
   return SPX_OK;
 }
@@ -172,6 +214,68 @@ void launch_ratio(spx_ctx* ctx) {
                      ctx->nbn, ctx->ratio_part, ctx->basis, ctx->prm, ctx->st);
 }
 
+constexpr int LOOP_MAX = 16;
+struct PtrArr {
+  double* p[LOOP_MAX];
+};
+
+__global__ __launch_bounds__(BLK) void loop_sum_kernel(PtrArr srcs, int nsrc,
+                                                       double* __restrict__ dst, int64_t n) {
+  const int64_t j = (int64_t)blockIdx.x * BLK + threadIdx.x;
+  if (j >= n) return;
+  double s = 0.0;
+  for (int q = 0; q < nsrc; ++q) s += srcs.p[q][j];
+  dst[j] = s;
+}
+
+int loop_fail(spx_ctx* ctx) {
+  ctx->err = "loopback group barrier timed out (a peer rank stopped)";
+  return SPX_E_STATE;
+}
+
+// Publish on my stream, meet the peers, make my stream wait for theirs.
+int loop_meet(spx_ctx* ctx, hipEvent_t spx_ctx::*ev) {
+  LoopGroup* G = ctx->loop;
+  HIPC(hipEventRecord(ctx->*ev, ctx->stream));
+  if (!G->barrier()) return loop_fail(ctx);
+  for (int q = 0; q < G->n; ++q) HIPC(hipStreamWaitEvent(ctx->stream, G->members[q]->*ev, 0));
+  return SPX_OK;
+}
+
+int comm_allgather_keys(spx_ctx* ctx) {
+  if (ctx->comm) {
+    NCCLC(ncclAllGather(ctx->sendkey, ctx->keys_all, sizeof(Key), ncclUint8, ctx->comm,
+                        ctx->stream));
+    return SPX_OK;
+  }
+  LoopGroup* G = ctx->loop;
+  int rc = loop_meet(ctx, &spx_ctx::ev_ready);
+  if (rc) return rc;
+  for (int q = 0; q < G->n; ++q)
+    HIPC(hipMemcpyAsync(ctx->keys_all + q, G->members[q]->sendkey, sizeof(Key),
+                        hipMemcpyDeviceToDevice, ctx->stream));
+  return loop_meet(ctx, &spx_ctx::ev_done);  // peers' sendkey reusable after this
+}
+
+int comm_allreduce_p(spx_ctx* ctx) {
+  if (ctx->comm) {
+    NCCLC(ncclAllReduce(ctx->P, ctx->P, (size_t)ctx->N, ncclDouble, ncclSum, ctx->comm,
+                        ctx->stream));
+    return SPX_OK;
+  }
+  LoopGroup* G = ctx->loop;
+  int rc = loop_meet(ctx, &spx_ctx::ev_ready);
+  if (rc) return rc;
+  PtrArr a;
+  for (int q = 0; q < G->n; ++q) a.p[q] = G->members[q]->P;
+  hipLaunchKernelGGL(loop_sum_kernel, dim3(ctx->nbn), dim3(BLK), 0, ctx->stream, a, G->n,
+                     ctx->Ptmp, ctx->N);
+  if ((rc = loop_meet(ctx, &spx_ctx::ev_done))) return rc;  // peers finished reading my P
+  HIPC(hipMemcpyAsync(ctx->P, ctx->Ptmp, sizeof(double) * ctx->N, hipMemcpyDeviceToDevice,
+                      ctx->stream));
+  return SPX_OK;
+}
+
 // Enqueue one pivot (all launches on ctx->stream; no host synchronisation).
 int enqueue_pivot(spx_ctx* ctx, bool time_elim) {
   launch_ratio(ctx);
@@ -180,11 +284,10 @@ int enqueue_pivot(spx_ctx* ctx, bool time_elim) {
   } else {
     hipLaunchKernelGGL(select_kernel, dim3(1), dim3(BLK), 0, ctx->stream, ctx->ratio_part,
                        ctx->nbr, ctx->sendkey, ctx->st);
-    NCCLC(ncclAllGather(ctx->sendkey, ctx->keys_all, sizeof(Key), ncclUint8, ctx->comm,
-                        ctx->stream));
+    int rc = comm_allgather_keys(ctx);
+    if (rc) return rc;
     launch_norm<MODE_PROW>(ctx, ctx->keys_all, ctx->nranks);
-    NCCLC(ncclAllReduce(ctx->P, ctx->P, (size_t)ctx->N, ncclDouble, ncclSum, ctx->comm,
-                        ctx->stream));
+    if ((rc = comm_allreduce_p(ctx))) return rc;
     launch_norm<MODE_FINISH>(ctx, nullptr, 0);
   }
   if (time_elim) {
@@ -309,6 +412,7 @@ int alloc_common(spx_ctx* ctx, int64_t m_local, int64_t N, int64_t m_global, int
   HIPC(hipMalloc(&ctx->ratio_part, sizeof(Key) * ctx->nbr));
   HIPC(hipMalloc(&ctx->sendkey, sizeof(Key)));
   HIPC(hipMalloc(&ctx->keys_all, sizeof(Key) * ctx->nranks));
+  if (ctx->loop) HIPC(hipMalloc(&ctx->Ptmp, sizeof(double) * N));
   HIPC(hipMemsetAsync(ctx->A, 0, sizeof(double) * ctx->ld * N, ctx->stream));
   HIPC(hipMemsetAsync(ctx->F, 0, sizeof(double) * ctx->ld, ctx->stream));
   HIPC(hipMemsetAsync(ctx->P, 0, sizeof(double) * N, ctx->stream));
@@ -386,8 +490,54 @@ int spx_create_sharded(spx_ctx** out, int device, int rank, int nranks, const ch
   return SPX_OK;
 }
 
+static std::mutex g_loop_mu;  // guards the registry of in-process groups only
+static std::map<std::string, LoopGroup*> g_loops;
+
+int spx_create_sharded_local(spx_ctx** out, int device, int rank, int nranks,
+                             const char id[128]) {
+  int rc = spx_create(out, device);
+  if (rc) return rc;
+  spx_ctx* ctx = *out;
+  CHECK_ARG(nranks >= 1 && nranks <= LOOP_MAX && rank >= 0 && rank < nranks && id,
+            "bad rank/nranks/id (loopback groups hold at most 16 ranks)");
+  ctx->rank = rank;
+  ctx->nranks = nranks;
+  ctx->sharded = true;
+  HIPC(hipEventCreateWithFlags(&ctx->ev_ready, hipEventDisableTiming));
+  HIPC(hipEventCreateWithFlags(&ctx->ev_done, hipEventDisableTiming));
+  std::lock_guard<std::mutex> lk(g_loop_mu);
+  const std::string key(id, 128);
+  LoopGroup*& G = g_loops[key];
+  if (!G) {
+    G = new LoopGroup();
+    G->n = nranks;
+    G->key = key;
+    G->members.assign(nranks, nullptr);
+  }
+  if (G->n != nranks || G->members[rank] != nullptr) {
+    ctx->err = "loopback group: rank taken or size mismatch";
+    return SPX_E_ARG;
+  }
+  G->members[rank] = ctx;
+  G->refs++;
+  ctx->loop = G;
+  return SPX_OK;
+}
+
 int spx_destroy(spx_ctx* ctx) {
   if (!ctx) return SPX_OK;
+  if (ctx->loop) {
+    std::lock_guard<std::mutex> lk(g_loop_mu);
+    LoopGroup* G = ctx->loop;
+    G->members[ctx->rank] = nullptr;
+    if (--G->refs == 0) {
+      g_loops.erase(G->key);
+      delete G;
+    }
+    ctx->loop = nullptr;
+  }
+  if (ctx->ev_ready) (void)hipEventDestroy(ctx->ev_ready);
+  if (ctx->ev_done) (void)hipEventDestroy(ctx->ev_done);
   (void)hipSetDevice(ctx->device);
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
   free_buffers(ctx);
@@ -557,7 +707,7 @@ int spx_solve(spx_ctx* ctx, const spx_opts* opts, spx_result* res) {
   if (rc) return rc;
   const int64_t it0 = ctx->h_st->iters;
   const int chunk = o->chunk > 0 ? o->chunk : 32;
-  bool use_graph = o->use_graph != 0;
+  const bool use_graph = o->use_graph != 0 && !ctx->loop;
   if (use_graph) {
     rc = build_graph(ctx, chunk);
     if (rc) return rc;
@@ -575,7 +725,7 @@ int spx_solve(spx_ctx* ctx, const spx_opts* opts, spx_result* res) {
     if (status != SPX_RUNNING) break;
     const double el =
         std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-    if (o->time_limit_s > 0 && el >= o->time_limit_s) {
+    if (o->time_limit_s > 0 && el >= o->time_limit_s && !ctx->sharded) {
       status = SPX_ITER_LIMIT;
       break;
     }
@@ -637,7 +787,7 @@ int spx_run_pivots(spx_ctx* ctx, const spx_opts* opts, int64_t npivots, int time
   const spx_opts* o = opts ? opts : &d;
   int rc = begin_call(ctx, o);
   if (rc) return rc;
-  if (!time_elim && o->use_graph) {
+  if (!time_elim && o->use_graph && !ctx->loop) {
     const int chunk = o->chunk > 0 ? o->chunk : 32;
     if ((rc = build_graph(ctx, chunk))) return rc;
     int64_t left = npivots;

@@ -75,6 +75,8 @@ SIGNATURES = {
     "spx_comm_unique_id": (ctypes.c_int, [ctypes.c_char_p]),
     "spx_create_sharded": (ctypes.c_int, [ctypes.POINTER(_P), ctypes.c_int, ctypes.c_int,
                                           ctypes.c_int, ctypes.c_char_p]),
+    "spx_create_sharded_local": (ctypes.c_int, [ctypes.POINTER(_P), ctypes.c_int, ctypes.c_int,
+                                                ctypes.c_int, ctypes.c_char_p]),
     "spx_load": (ctypes.c_int, [_P, _DP, _I64, _I64, _I64, ctypes.c_int, _LP]),
     "spx_load_rows": (ctypes.c_int, [_P, _DP, _I64, _I64, _I64, ctypes.c_int, _DP, _LP, _I64,
                                      _I64]),

@@ -57,8 +57,10 @@ def exchange_unique_id(make_id=make_unique_id, group=None) -> bytes:
 class ShardedTableau(DeviceTableau):
     """This rank's row block of a tableau sharded over `world` GPUs."""
 
-    def __init__(self, device: int, rank: int, world: int, uid: bytes):
-        super().__init__(device, _sharded=(rank, world, uid))
+    def __init__(self, device: int, rank: int, world: int, uid: bytes, local: bool = False):
+        """local=True: the ranks are threads of this process sharing GPUs
+        (in-process loopback exchange instead of RCCL; for tests)."""
+        super().__init__(device, _sharded=(rank, world, uid, local))
         self.rank, self.world = rank, world
 
     @classmethod

@@ -76,9 +76,9 @@ class DeviceTableau:
         if _sharded is None:
             rc = self._lib.spx_create(ctypes.byref(self._ctx), int(device))
         else:
-            rank, nranks, uid = _sharded
-            rc = self._lib.spx_create_sharded(ctypes.byref(self._ctx), int(device), int(rank),
-                                              int(nranks), uid)
+            rank, nranks, uid, local = _sharded
+            create = self._lib.spx_create_sharded_local if local else self._lib.spx_create_sharded
+            rc = create(ctypes.byref(self._ctx), int(device), int(rank), int(nranks), uid)
         if rc != 0:
             msg = self._err()
             self.close()

@@ -314,3 +314,51 @@ def test_config3_size_first_pivots_bit_exact(eng_cls):
             col = e.column(int(b[k]))
             assert col[k] == 1.0 and np.count_nonzero(col) == 1  # basic columns = e_k
         assert e.column(m + n).min() >= -1e-9  # RHS stays feasible
+
+
+# ----------------------------------------------------------- sharded, nranks > 1
+def _sharded_threads(world, kind, m, n, seed, rule, **solve_kw):
+    from simplex_amd import dist, synth
+    uid = bytes([world, m % 251, n % 251, seed % 251]) + os.urandom(124)
+    outs, errors = {}, []
+
+    def rank_main(rank):
+        try:
+            r0, r1 = dist.row_partition(m, world, rank)
+            T, obj, basis = synth.tableau_rows(kind, m, n, seed, r0, r1, order="F")
+            with dist.ShardedTableau(0, rank, world, uid, local=True) as s:
+                s.load_shard(T, obj, basis, m, r0)
+                res = s.solve(rule=rule, **solve_kw)
+                outs[rank] = (r0, r1, res, s.history().tolist(), s.tableau(), s.basis())
+        except Exception as ex:  # pragma: no cover
+            errors.append(ex)
+
+    th = [threading.Thread(target=rank_main, args=(r,)) for r in range(world)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=600)
+    assert not errors, errors
+    return outs
+
+
+@pytest.mark.parametrize("world,kind,m,n,rule", [
+    (2, "dense", 200, 300, "dantzig"),
+    (3, "dense", 301, 257, "dantzig"),
+    (4, "dense", 1024, 2048, "dantzig"),
+    (2, "degenerate", 64, 64, "bland"),
+    (5, "dense", 7, 9, "dantzig"),   # ranks with one or two rows
+])
+def test_sharded_virtual_ranks_bit_exact(world, kind, m, n, rule):
+    """nranks > 1 sharded kernels (select / PROW / FINISH, row offsets,
+    owner vs non-owner ranks) on one GPU through the in-process exchange."""
+    from simplex_amd import synth
+    outs = _sharded_threads(world, kind, m, n, 3, rule)
+    T, basis = synth.full_tableau(kind, m, n, 3)
+    st, hist = O.solve_tableau(T, basis, rule=rule, max_iters=200000)
+    for rank, (r0, r1, res, h, Tl, b) in outs.items():
+        assert res.status == st
+        assert [tuple(x) for x in h] == hist
+        assert np.array_equal(Tl[:-1], T[r0:r1])
+        assert np.array_equal(Tl[-1], T[-1])
+        assert np.array_equal(b, basis)
