@@ -156,8 +156,10 @@ int spx_state(spx_ctx* ctx, int32_t* status, int64_t* iters, double* objective);
 int spx_elim_timing(spx_ctx* ctx, double* total_ms, int64_t* count, int64_t* touched_cols,
                     int reset);
 
-/* Tuning knob: 1 = non-temporal loads/stores in the elimination stream. */
+/* Tuning knobs: 1 = non-temporal loads/stores in the elimination stream;
+ * elimination rows per thread R (2, 4, 8; 0 = auto) and grid target. */
 int spx_set_elim_nt(spx_ctx* ctx, int nt);
+int spx_set_elim_geometry(spx_ctx* ctx, int R, int target_wgs);
 
 #ifdef __cplusplus
 }

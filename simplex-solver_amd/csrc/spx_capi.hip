@@ -104,6 +104,8 @@ struct spx_ctx {
   // launch geometry
   int nbn = 1, nbr = 1, rch = 1, G = 1, R = 8;
   int elim_nt = 0;
+  int tune_R = 0;          // 0: automatic
+  int tune_wgs = 0;        // 0: automatic (2048)
 
   // graph cache
   hipGraphExec_t gexec = nullptr;
@@ -175,9 +177,10 @@ int64_t round_up(int64_t x, int64_t a) { return (x + a - 1) / a * a; }
 void choose_geometry(spx_ctx* ctx) {
   const int64_t m = ctx->m_local;
   ctx->R = (m >= 4096) ? 8 : (m >= 1024 ? 4 : 2);
+  if (ctx->tune_R == 2 || ctx->tune_R == 4 || ctx->tune_R == 8) ctx->R = ctx->tune_R;
   const int64_t rc = (int64_t)BLK * ctx->R;
   ctx->rch = (int)std::max<int64_t>(1, (m + rc - 1) / rc);
-  const int target = 2048;  // 256 CUs x 8 workgroups
+  const int target = ctx->tune_wgs > 0 ? ctx->tune_wgs : 2048;  // 256 CUs x 8 workgroups
   ctx->G = std::max(1, target / ctx->rch);
   ctx->G = (int)std::min<int64_t>(ctx->G, std::max<int64_t>(1, ctx->N));
   ctx->nbn = (int)std::max<int64_t>(1, (ctx->N + BLK - 1) / BLK);
@@ -841,6 +844,18 @@ int spx_elim_timing(spx_ctx* ctx, double* total_ms, int64_t* count, int64_t* tou
     ctx->ev_used = 0;
     ctx->touched_at_reset = ctx->h_st->touched_total;
   }
+  return SPX_OK;
+}
+
+// Tuning knob: elimination rows per thread (2/4/8, 0 = auto) and target grid size.
+int spx_set_elim_geometry(spx_ctx* ctx, int R, int target_wgs) {
+  if (!ctx) return SPX_E_ARG;
+  ctx->tune_R = R;
+  ctx->tune_wgs = target_wgs;
+  if (ctx->loaded) choose_geometry(ctx);
+  if (ctx->gexec) (void)hipGraphExecDestroy(ctx->gexec);
+  ctx->gexec = nullptr;
+  ctx->gchunk = 0;
   return SPX_OK;
 }
 

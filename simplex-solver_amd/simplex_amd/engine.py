@@ -249,5 +249,9 @@ class DeviceTableau:
                     "spx_elim_timing")
         return float(ms.value), int(cnt.value), int(cols.value)
 
+    def set_elim_geometry(self, R: int = 0, target_wgs: int = 0) -> None:
+        self._check(self._lib.spx_set_elim_geometry(self._ctx, int(R), int(target_wgs)),
+                    "spx_set_elim_geometry")
+
     def set_elim_nt(self, nt: bool) -> None:
         self._check(self._lib.spx_set_elim_nt(self._ctx, 1 if nt else 0), "spx_set_elim_nt")
