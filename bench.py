@@ -41,7 +41,11 @@ def parse():
     ap.add_argument("--seed", type=int, default=20251205)
     ap.add_argument("--rule", default="dantzig")
     ap.add_argument("--dense", action="store_true", help="dense sweep (no zero-column skip)")
-    ap.add_argument("--nt", action="store_true", help="non-temporal elimination stream")
+    ap.add_argument("--nt", type=int, default=-1,
+                    help="elim non-temporal flags: 1 loads, 2 stores (-1: engine default)")
+    ap.add_argument("--ilv", type=int, default=-1, help="elim interleaved columns (-1: default)")
+    ap.add_argument("--R", type=int, default=0, help="elim rows per thread (0: auto)")
+    ap.add_argument("--wgs", type=int, default=0, help="elim grid target (0: auto)")
     ap.add_argument("--graph", type=int, default=-1,
                     help="1: time hipGraph replays (elim events in a separate window); "
                          "0: direct launches with per-elim events; -1: auto (N>1 -> 1)")
@@ -122,7 +126,8 @@ def main():
     Tf, obj, basis = synth.tableau_rows("dense", m, n, args.seed, row0, row1, order="F")
     eng.load_rows(Tf, obj, basis, m, row0)
     del Tf
-    eng.set_elim_nt(args.nt)
+    if args.nt >= 0 or args.ilv >= 0 or args.R or args.wgs:
+        eng.set_elim_variant(args.R, args.wgs, max(args.nt, 0), args.ilv > 0)
     opts = dict(rule=args.rule, skip_zero_cols=not args.dense, use_graph=True, chunk=32)
 
     def barrier():

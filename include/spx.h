@@ -156,10 +156,10 @@ int spx_state(spx_ctx* ctx, int32_t* status, int64_t* iters, double* objective);
 int spx_elim_timing(spx_ctx* ctx, double* total_ms, int64_t* count, int64_t* touched_cols,
                     int reset);
 
-/* Tuning knobs: 1 = non-temporal loads/stores in the elimination stream;
- * elimination rows per thread R (2, 4, 8; 0 = auto) and grid target. */
-int spx_set_elim_nt(spx_ctx* ctx, int nt);
-int spx_set_elim_geometry(spx_ctx* ctx, int R, int target_wgs);
+/* Tuning knob of the elimination kernel: rows per thread R (2, 4, 8; 0 = auto),
+ * grid target (0 = auto), non-temporal flags (bit 0 loads, bit 1 stores) and
+ * interleaved column assignment (1) instead of contiguous column ranges (0). */
+int spx_set_elim_variant(spx_ctx* ctx, int R, int target_wgs, int nt_flags, int interleave);
 
 #ifdef __cplusplus
 }

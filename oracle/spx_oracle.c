@@ -1,0 +1,123 @@
+/*
+ * spx_oracle.c — C restatement of the tableau simplex spec.
+ * TEST INFRASTRUCTURE ONLY: used by tests/ as a second checker and by
+ * bench.py's cpu_baseline leg as the multi-core CPU baseline.  Never linked
+ * into or called by the product (simplex-solver_amd/).
+ *
+ * Same rules as oracle/simplex_oracle.py (which restates the pivot loop of the
+ * third-party simple_simplex engine driven at reference
+ * app/controllers/solver_controller.py:290-319; parity with that package is
+ * UNPINNED):
+ *   enter : Dantzig argmin (z_j, j) over j < n_enter with z_j < -eps_opt;
+ *           Bland smallest such j.
+ *   leave : rows with T[i,c] > eps_piv; min (T[i,rhs]/T[i,c], tie) with
+ *           tie = i (Dantzig) or basis[i] (Bland); NaN ratios ignored.
+ *   pivot : p = T[r,:]/T[r,c]; columns with p[j] != 0 (all if !skip_zero):
+ *           T[i,j] = T[i,j] - f[i]*p[j] (rounded product, rounded difference),
+ *           row r = p; column c = e_r.
+ * Layout: row-major (m+1) x N, objective row last.  Compile with
+ * -ffp-contract=off (no FMA) so the results are bit-identical.
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+int spxo_threads(void) {
+#ifdef _OPENMP
+  return omp_get_max_threads();
+#else
+  return 1;
+#endif
+}
+
+int64_t spxo_enter(const double* z, int64_t n_enter, int rule, double eps_opt) {
+  int64_t best = -1;
+  for (int64_t j = 0; j < n_enter; ++j) {
+    if (!(z[j] < -eps_opt)) continue;
+    if (rule == 1) return j;
+    if (best < 0 || z[j] < z[best]) best = j;
+  }
+  return best;
+}
+
+int64_t spxo_leave(const double* T, int64_t rows, int64_t cols, int64_t c, const int64_t* basis,
+                   int rule, double eps_piv) {
+  const int64_t m = rows - 1;
+  int64_t best = -1;
+  double bv = 0.0;
+  int64_t bt = 0;
+  for (int64_t i = 0; i < m; ++i) {
+    const double a = T[i * cols + c];
+    if (!(a > eps_piv)) continue;
+    const double q = T[i * cols + cols - 1] / a;
+    if (isnan(q)) continue;
+    const int64_t t = rule == 1 ? basis[i] : i;
+    if (best < 0 || q < bv || (q == bv && t < bt)) {
+      best = i;
+      bv = q;
+      bt = t;
+    }
+  }
+  return best;
+}
+
+void spxo_pivot(double* T, int64_t rows, int64_t cols, int64_t r, int64_t c, int skip_zero) {
+  double* p = (double*)malloc(sizeof(double) * cols);
+  double* f = (double*)malloc(sizeof(double) * rows);
+  const double piv = T[r * cols + c];
+  for (int64_t j = 0; j < cols; ++j) p[j] = T[r * cols + j] / piv;
+  for (int64_t i = 0; i < rows; ++i) f[i] = T[i * cols + c];
+#pragma omp parallel for schedule(static)
+  for (int64_t i = 0; i < rows; ++i) {
+    double* row = T + i * cols;
+    if (i == r) {
+      for (int64_t j = 0; j < cols; ++j)
+        if (!skip_zero || p[j] != 0.0) row[j] = p[j];
+    } else {
+      const double fi = f[i];
+      for (int64_t j = 0; j < cols; ++j) {
+        const double prod = fi * p[j];
+        const double upd = row[j] - prod;
+        row[j] = (!skip_zero || p[j] != 0.0) ? upd : row[j];
+      }
+    }
+    row[c] = (i == r) ? 1.0 : 0.0;
+  }
+  free(p);
+  free(f);
+}
+
+/* Returns 0 optimal, 1 iteration limit, 3 unbounded; hist gets (r,c) pairs. */
+int spxo_solve(double* T, int64_t rows, int64_t cols, int64_t* basis, int rule, double eps_opt,
+               double eps_piv, int64_t n_enter, int64_t max_iters, int skip_zero,
+               int64_t* hist, int64_t hist_cap, int64_t* n_piv) {
+  int64_t k = 0;
+  if (n_enter <= 0 || n_enter > cols - 1) n_enter = cols - 1;
+  for (;;) {
+    if (max_iters > 0 && k >= max_iters) {
+      *n_piv = k;
+      return 1;
+    }
+    const int64_t c = spxo_enter(T + (rows - 1) * cols, n_enter, rule, eps_opt);
+    if (c < 0) {
+      *n_piv = k;
+      return 0;
+    }
+    const int64_t r = spxo_leave(T, rows, cols, c, basis, rule, eps_piv);
+    if (r < 0) {
+      *n_piv = k;
+      return 3;
+    }
+    spxo_pivot(T, rows, cols, r, c, skip_zero);
+    basis[r] = c;
+    if (k < hist_cap) {
+      hist[2 * k] = r;
+      hist[2 * k + 1] = c;
+    }
+    ++k;
+  }
+}

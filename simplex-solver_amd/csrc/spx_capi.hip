@@ -2,10 +2,12 @@
 //
 // Host runtime: one context = one HIP stream + the device-resident tableau,
 // pivot vectors, reduction partials and a device State block.  The pivot loop
-// never round-trips to the host inside a chunk: each pivot is three kernels
-// (ratio -> norm -> elim), and chunks of `chunk` pivots are captured once into
-// a hipGraph and replayed; the host only reads the 80-byte State (pinned) after
-// each chunk to check for termination / limits.
+// never round-trips to the host inside a chunk: each host call primes the
+// first pivot (norm<INIT> + prime_kernel), then every pivot is two kernels
+// (norm -> elim, the elim also running the next pivot's ratio test), and
+// chunks of `chunk` pivots are captured once into a hipGraph and replayed; the
+// host only reads the State block (pinned) after each chunk to check for
+// termination / limits.
 //
 // Sharded contexts (spx_create_sharded) split the constraint rows across ranks,
 // one process per GPU.  Per pivot they add one RCCL all-gather of a 32-B
@@ -87,7 +89,7 @@ struct spx_ctx {
   // device buffers
   double* A = nullptr;     // ld * N, column-major local rows
   double* obj = nullptr;   // N
-  double* F = nullptr;     // ld   pivot-column snapshot
+  double* F = nullptr;     // 2*ld pivot-column snapshots (by pivot parity)
   double* P = nullptr;     // N    pivot row (normalised)
   int* list = nullptr;     // N    compacted columns
   int64_t* basis = nullptr;// m_global
@@ -103,7 +105,8 @@ struct spx_ctx {
 
   // launch geometry
   int nbn = 1, nbr = 1, rch = 1, G = 1, R = 8;
-  int elim_nt = 0;
+  int elim_nt = 0;         // bit 0: non-temporal loads, bit 1: non-temporal stores
+  int elim_ilv = 0;        // interleaved column assignment
   int tune_R = 0;          // 0: automatic
   int tune_wgs = 0;        // 0: automatic (2048)
 
@@ -187,19 +190,34 @@ void choose_geometry(spx_ctx* ctx) {
   ctx->nbr = (int)std::min<int64_t>(256, std::max<int64_t>(1, (m + 2 * BLK - 1) / (2 * BLK)));
 }
 
-template <int R, bool NT>
+template <int R, bool NTL, bool NTS, bool ILV>
 void launch_elim_t(spx_ctx* ctx) {
-  hipLaunchKernelGGL((elim_kernel<R, NT>), dim3(ctx->rch * ctx->G), dim3(BLK), 0, ctx->stream,
-                     ctx->A, ctx->ld, ctx->m_local, ctx->row0, ctx->F, ctx->P, ctx->list,
-                     ctx->rch, ctx->G, ctx->st);
+  hipLaunchKernelGGL((elim_kernel<R, NTL, NTS, ILV>), dim3(ctx->rch * ctx->G), dim3(BLK), 0,
+                     ctx->stream, ctx->A, ctx->ld, ctx->m_local, ctx->row0, ctx->N, ctx->F,
+                     ctx->P, ctx->list, ctx->rch, ctx->G, ctx->enter_part, ctx->nbn,
+                     ctx->ratio_part, ctx->obj, ctx->basis, ctx->prm, ctx->st);
+}
+
+template <int R>
+void launch_elim_r(spx_ctx* ctx) {
+  const int v = (ctx->elim_nt & 3) | (ctx->elim_ilv ? 4 : 0);
+  switch (v) {
+    case 0: launch_elim_t<R, false, false, false>(ctx); break;
+    case 1: launch_elim_t<R, true, false, false>(ctx); break;
+    case 2: launch_elim_t<R, false, true, false>(ctx); break;
+    case 3: launch_elim_t<R, true, true, false>(ctx); break;
+    case 4: launch_elim_t<R, false, false, true>(ctx); break;
+    case 5: launch_elim_t<R, true, false, true>(ctx); break;
+    case 6: launch_elim_t<R, false, true, true>(ctx); break;
+    default: launch_elim_t<R, true, true, true>(ctx); break;
+  }
 }
 
 void launch_elim(spx_ctx* ctx) {
-  const bool nt = ctx->elim_nt != 0;
   switch (ctx->R) {
-    case 8: nt ? launch_elim_t<8, true>(ctx) : launch_elim_t<8, false>(ctx); break;
-    case 4: nt ? launch_elim_t<4, true>(ctx) : launch_elim_t<4, false>(ctx); break;
-    default: nt ? launch_elim_t<2, true>(ctx) : launch_elim_t<2, false>(ctx); break;
+    case 8: launch_elim_r<8>(ctx); break;
+    case 4: launch_elim_r<4>(ctx); break;
+    default: launch_elim_r<2>(ctx); break;
   }
 }
 
@@ -211,8 +229,8 @@ void launch_norm(spx_ctx* ctx, const Key* keys, int nkeys) {
                      ctx->st);
 }
 
-void launch_ratio(spx_ctx* ctx) {
-  hipLaunchKernelGGL(ratio_kernel, dim3(ctx->nbr), dim3(BLK), 0, ctx->stream, ctx->A, ctx->ld,
+void launch_prime(spx_ctx* ctx) {
+  hipLaunchKernelGGL(prime_kernel, dim3(ctx->nbr), dim3(BLK), 0, ctx->stream, ctx->A, ctx->ld,
                      ctx->m_local, ctx->row0, ctx->N, ctx->obj, ctx->F, ctx->enter_part,
                      ctx->nbn, ctx->ratio_part, ctx->basis, ctx->prm, ctx->st);
 }
@@ -281,12 +299,11 @@ int comm_allreduce_p(spx_ctx* ctx) {
 
 // Enqueue one pivot (all launches on ctx->stream; no host synchronisation).
 int enqueue_pivot(spx_ctx* ctx, bool time_elim) {
-  launch_ratio(ctx);
   if (!ctx->sharded) {
-    launch_norm<MODE_FUSED>(ctx, ctx->ratio_part, ctx->nbr);
+    launch_norm<MODE_FUSED>(ctx, ctx->ratio_part, 0);
   } else {
     hipLaunchKernelGGL(select_kernel, dim3(1), dim3(BLK), 0, ctx->stream, ctx->ratio_part,
-                       ctx->nbr, ctx->sendkey, ctx->st);
+                       ctx->sendkey, ctx->st);
     int rc = comm_allgather_keys(ctx);
     if (rc) return rc;
     launch_norm<MODE_PROW>(ctx, ctx->keys_all, ctx->nranks);
@@ -342,8 +359,9 @@ int pull_state(spx_ctx* ctx) {
   return SPX_OK;
 }
 
-// Prepare a pivot call: params, status RUNNING, fresh entering partials.
-int begin_call(spx_ctx* ctx, const spx_opts* o) {
+// Prepare a pivot call: params, status RUNNING, fresh entering partials and
+// the primed first pivot (rule-chosen, or the forced (fr, fc) of spx_pivot_at).
+int begin_call(spx_ctx* ctx, const spx_opts* o, int64_t fc = -1, int64_t fr = -1) {
   if (!ctx->loaded) {
     ctx->err = "no tableau loaded";
     return SPX_E_STATE;
@@ -351,8 +369,9 @@ int begin_call(spx_ctx* ctx, const spx_opts* o) {
   int rc = pull_state(ctx);
   if (rc) return rc;
   if ((rc = write_params(ctx, o))) return rc;
-  if ((rc = set_state_fields(ctx, ST_RUNNING, -1, -1))) return rc;
+  if ((rc = set_state_fields(ctx, ST_RUNNING, fc, fr))) return rc;
   launch_norm<MODE_INIT>(ctx, nullptr, 0);
+  launch_prime(ctx);
   HIPC(hipGetLastError());
   return SPX_OK;
 }
@@ -406,18 +425,18 @@ int alloc_common(spx_ctx* ctx, int64_t m_local, int64_t N, int64_t m_global, int
   HIPC(hipSetDevice(ctx->device));
   HIPC(hipMalloc(&ctx->A, sizeof(double) * ctx->ld * N));
   HIPC(hipMalloc(&ctx->obj, sizeof(double) * N));
-  HIPC(hipMalloc(&ctx->F, sizeof(double) * ctx->ld));
+  HIPC(hipMalloc(&ctx->F, sizeof(double) * 2 * ctx->ld));
   HIPC(hipMalloc(&ctx->P, sizeof(double) * N));
   HIPC(hipMalloc(&ctx->list, sizeof(int) * N));
   HIPC(hipMalloc(&ctx->basis, sizeof(int64_t) * std::max<int64_t>(1, m_global)));
   HIPC(hipMalloc(&ctx->hist, sizeof(int64_t) * 2 * ctx->hist_cap));
   HIPC(hipMalloc(&ctx->enter_part, sizeof(Key) * ctx->nbn));
-  HIPC(hipMalloc(&ctx->ratio_part, sizeof(Key) * ctx->nbr));
+  HIPC(hipMalloc(&ctx->ratio_part, sizeof(Key) * std::max(ctx->nbr, ctx->rch)));
   HIPC(hipMalloc(&ctx->sendkey, sizeof(Key)));
   HIPC(hipMalloc(&ctx->keys_all, sizeof(Key) * ctx->nranks));
   if (ctx->loop) HIPC(hipMalloc(&ctx->Ptmp, sizeof(double) * N));
   HIPC(hipMemsetAsync(ctx->A, 0, sizeof(double) * ctx->ld * N, ctx->stream));
-  HIPC(hipMemsetAsync(ctx->F, 0, sizeof(double) * ctx->ld, ctx->stream));
+  HIPC(hipMemsetAsync(ctx->F, 0, sizeof(double) * 2 * ctx->ld, ctx->stream));
   HIPC(hipMemsetAsync(ctx->P, 0, sizeof(double) * N, ctx->stream));
   std::memset(ctx->h_st, 0, sizeof(State));
   ctx->h_st->status = ST_RUNNING;
@@ -770,9 +789,8 @@ int spx_pivot_at(spx_ctx* ctx, int64_t r, int64_t c) {
   if (!ctx) return SPX_E_ARG;
   CHECK_ARG(ctx->loaded && r >= 0 && r < ctx->m_global && c >= 0 && c < ctx->N - 1,
             "pivot position out of range");
-  int rc = begin_call(ctx, nullptr);
+  int rc = begin_call(ctx, nullptr, c, r);
   if (rc) return rc;
-  if ((rc = set_state_fields(ctx, ST_RUNNING, c, r))) return rc;
   if ((rc = enqueue_pivot(ctx, false))) return rc;
   // pull the post-pivot state before writing the forced fields back
   if ((rc = pull_state(ctx))) return rc;
@@ -847,27 +865,25 @@ int spx_elim_timing(spx_ctx* ctx, double* total_ms, int64_t* count, int64_t* tou
   return SPX_OK;
 }
 
-// Tuning knob: elimination rows per thread (2/4/8, 0 = auto) and target grid size.
-int spx_set_elim_geometry(spx_ctx* ctx, int R, int target_wgs) {
+// Tuning knob: elimination rows per thread R (2/4/8, 0 = auto), grid target
+// (0 = auto), non-temporal flags (bit 0 loads, bit 1 stores), interleaved
+// column assignment.
+int spx_set_elim_variant(spx_ctx* ctx, int R, int target_wgs, int nt_flags, int interleave) {
   if (!ctx) return SPX_E_ARG;
   ctx->tune_R = R;
   ctx->tune_wgs = target_wgs;
-  if (ctx->loaded) choose_geometry(ctx);
+  ctx->elim_nt = nt_flags & 3;
+  ctx->elim_ilv = interleave ? 1 : 0;
+  if (ctx->loaded) {
+    choose_geometry(ctx);
+    if (ctx->rch > ctx->nbr) {  // ratio_part must hold rch partials
+      dfree(ctx->ratio_part);
+      HIPC(hipMalloc(&ctx->ratio_part, sizeof(Key) * std::max(ctx->nbr, ctx->rch)));
+    }
+  }
   if (ctx->gexec) (void)hipGraphExecDestroy(ctx->gexec);
   ctx->gexec = nullptr;
   ctx->gchunk = 0;
-  return SPX_OK;
-}
-
-// Tuning knob (not part of the stable ABI): non-temporal elimination stream.
-int spx_set_elim_nt(spx_ctx* ctx, int nt) {
-  if (!ctx) return SPX_E_ARG;
-  if ((nt != 0) != (ctx->elim_nt != 0)) {
-    ctx->elim_nt = nt;
-    if (ctx->gexec) (void)hipGraphExecDestroy(ctx->gexec);
-    ctx->gexec = nullptr;
-    ctx->gchunk = 0;
-  }
   return SPX_OK;
 }
 

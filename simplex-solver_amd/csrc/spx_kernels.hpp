@@ -2,17 +2,21 @@
 //
 // One pivot of the tableau method (the loop inside simple_simplex's
 // optimize_json_format, called at reference app/controllers/solver_controller.py:318)
-// is three launches on one stream:
+// is TWO launches on one stream in steady state:
 //
-//   ratio_kernel  : entering column c from the previous pivot's per-block
-//                   reduced-cost partials; pivot-column snapshot F = T[:,c];
-//                   per-block min-ratio partials over the constraint rows.
-//   norm_kernel   : leaving row r from the ratio partials; pivot row
-//                   p = T[r,:] / T[r,c]; objective-row update; compaction of
-//                   the columns with p[j] != 0; per-block entering partials
-//                   for the NEXT pivot; basis / history bookkeeping.
-//   elim_kernel   : T[i,j] <- T[i,j] - F[i]*p[j] over the compacted columns,
-//                   row r <- p, column c <- e_r.  The HBM-roofline kernel.
+//   norm_kernel  : leaving row r from the ratio partials; pivot row
+//                  p = T[r,:] / T[r,c]; objective-row update; compaction of the
+//                  columns with p[j] != 0; per-block entering partials for the
+//                  NEXT pivot; basis / history bookkeeping.
+//   elim_kernel  : T[i,j] <- T[i,j] - F[i]*p[j] over the compacted columns,
+//                  row r <- p, column c <- e_r (the HBM-roofline kernel), and,
+//                  fused in, the NEXT pivot's ratio test: every block reduces
+//                  the entering partials to c'; column group 0 updates columns
+//                  c' and RHS of its row chunk itself, snapshots F' = T[:,c']
+//                  and writes that chunk's min-ratio partial.
+//
+// prime_kernel runs once per host call (after a load / objective change /
+// forced pivot) to produce the first c, F and ratio partials.
 //
 // Memory layout: the m constraint rows are stored COLUMN-MAJOR
 // (column j is ld contiguous doubles), so the ratio test reads two contiguous
@@ -21,8 +25,8 @@
 // objective row lives in its own contiguous vector `obj`.
 //
 // Arithmetic is fixed to match the oracle bit for bit: IEEE division for p
-// and the ratios, separate multiply and subtract (the library is compiled with
-// -ffp-contract=off), lexicographic (value, tie) argmin reductions.
+// and the ratios, separate multiply and subtract (never contracted to FMA),
+// lexicographic (value, tie) argmin reductions held in registers.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -47,26 +51,34 @@ struct Params {
   double eps_opt;
   double eps_piv;
   int64_t n_enter;
-  int64_t iter_limit;  // absolute pivot count at which the ratio kernel stops
+  int64_t iter_limit;  // absolute pivot count at which norm_kernel stops
 };
 
+// Written by exactly one thread of one kernel per pivot, read by the next
+// kernels on the stream; no field is written while another block of the same
+// launch may still read it.
 struct State {
   int32_t status;
-  int32_t nz_count;       // columns compacted by norm_kernel for this pivot
-  int64_t iters;          // pivots since load
-  int64_t c;              // entering column of the current pivot
-  int64_t r;              // leaving row (global index) of the current pivot
+  int32_t n_ratio_part;   // valid ratio partials for the pending pivot
+  int32_t count[2];       // compacted-column counters, by pivot parity
+  int32_t cur;            // parity slot of the pivot being eliminated
+  int32_t pad;
+  int64_t iters;          // pivots completed since load (elim increments)
+  int64_t c;              // entering column of the pivot being eliminated
+  int64_t r;              // its leaving row (global index)
   double zc;              // objective-row entry of column c before the pivot
   double piv;             // pivot element (owner rank only)
-  int64_t forced_c;       // >= 0: spx_pivot_at column
-  int64_t forced_r;       // >= 0: spx_pivot_at row
-  int64_t touched_total;  // sum of nz_count over pivots (byte accounting)
+  int64_t c_next;         // pending entering column (-1: optimal)
+  double zc_next;
+  int64_t forced_c;       // >= 0: spx_pivot_at column (prime_kernel)
+  int64_t forced_r;       // >= 0: spx_pivot_at row (norm_kernel)
+  int64_t touched_total;  // sum of compacted columns over pivots (bytes)
   int64_t hist_cap;
 };
 
-// Lexicographic argmin key: smallest v, then smallest t.  `row` carries the
-// payload (leaving row / entering column).  t is unique among candidates, so
-// every reduction order gives the same answer.
+// Argmin key in memory (partials).  Smallest v, then smallest t; `row`
+// carries the payload.  t is unique among candidates, so every reduction
+// order gives the same answer.
 struct Key {
   double v;
   int64_t t;
@@ -74,67 +86,104 @@ struct Key {
   int64_t pad;
 };
 
-__device__ __forceinline__ Key key_none() {
-  Key k;
-  k.v = __builtin_inf();
-  k.t = INT64_MAX;
-  k.row = -1;
-  k.pad = 0;
-  return k;
+// The same key in registers: component-wise selects only (a select of the
+// whole struct made hipcc spill it to scratch).
+struct KeyR {
+  double v;
+  int64_t t;
+  int64_t row;
+};
+
+__device__ __forceinline__ KeyR keyr_none() { return KeyR{__builtin_inf(), INT64_MAX, -1}; }
+
+__device__ __forceinline__ void kmin(KeyR& a, double v, int64_t t, int64_t row) {
+  const bool take = (v < a.v) || (v == a.v && t < a.t);
+  a.v = take ? v : a.v;
+  a.t = take ? t : a.t;
+  a.row = take ? row : a.row;
 }
 
-__device__ __forceinline__ bool key_less(const Key& a, const Key& b) {
-  return (a.v < b.v) || (a.v == b.v && a.t < b.t);
-}
-
-__device__ __forceinline__ Key key_min(const Key& a, const Key& b) { return key_less(b, a) ? b : a; }
-
-__device__ __forceinline__ Key wave_min(Key k) {
+__device__ __forceinline__ void wave_min(KeyR& k) {
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) {
-    Key o;
-    o.v = __shfl_xor(k.v, off, 64);
-    o.t = __shfl_xor(k.t, off, 64);
-    o.row = __shfl_xor(k.row, off, 64);
-    o.pad = 0;
-    k = key_min(k, o);
+    const double v = __shfl_xor(k.v, off, 64);
+    const int64_t t = __shfl_xor(k.t, off, 64);
+    const int64_t row = __shfl_xor(k.row, off, 64);
+    kmin(k, v, t, row);
   }
-  return k;
 }
 
 // Block-wide argmin; every thread receives the result.
-__device__ __forceinline__ Key block_min(Key k) {
-  __shared__ Key sk[NWAVE];
-  k = wave_min(k);
+__device__ __forceinline__ KeyR block_min(KeyR k) {
+  __shared__ double sv[NWAVE];
+  __shared__ int64_t st_[NWAVE];
+  __shared__ int64_t sr[NWAVE];
+  wave_min(k);
   const int w = threadIdx.x >> 6;
-  if ((threadIdx.x & 63) == 0) sk[w] = k;
+  if ((threadIdx.x & 63) == 0) {
+    sv[w] = k.v;
+    st_[w] = k.t;
+    sr[w] = k.row;
+  }
   __syncthreads();
-  Key r = sk[0];
+  KeyR r{sv[0], st_[0], sr[0]};
 #pragma unroll
-  for (int i = 1; i < NWAVE; ++i) r = key_min(r, sk[i]);
+  for (int i = 1; i < NWAVE; ++i) kmin(r, sv[i], st_[i], sr[i]);
   __syncthreads();
   return r;
 }
 
-__device__ __forceinline__ Key reduce_keys(const Key* __restrict__ part, int n) {
-  Key k = key_none();
-  for (int i = threadIdx.x; i < n; i += BLK) k = key_min(k, part[i]);
+__device__ __forceinline__ KeyR reduce_keys(const Key* __restrict__ part, int n) {
+  KeyR k = keyr_none();
+  for (int i = threadIdx.x; i < n; i += BLK) kmin(k, part[i].v, part[i].t, part[i].row);
   return block_min(k);
 }
 
-// Explicit round-to-nearest multiply then subtract: never contracted to FMA.
+__device__ __forceinline__ void store_key(Key* dst, const KeyR& k) {
+  Key o;
+  o.v = k.v;
+  o.t = k.t;
+  o.row = k.row;
+  o.pad = 0;
+  *dst = o;
+}
+
+// Round-to-nearest multiply then subtract: never contracted to FMA.
 __device__ __forceinline__ double msub(double t, double f, double p) {
   return __dsub_rn(t, __dmul_rn(f, p));
 }
 
+// One candidate row of the min-ratio test.
+__device__ __forceinline__ void ratio_candidate(KeyR& k, double fv, double bv, int64_t grow,
+                                                const int64_t* __restrict__ basis, int32_t rule,
+                                                double eps_piv) {
+  if (fv > eps_piv) {
+    const double q = bv / fv;
+    if (q == q) kmin(k, q, (rule == RULE_BLAND) ? basis[grow] : grow, grow);
+  }
+}
+
+typedef double dbl2 __attribute__((ext_vector_type(2)));
+
+template <bool NT>
+__device__ __forceinline__ dbl2 ld2(const double* p) {
+  if (NT) return __builtin_nontemporal_load(reinterpret_cast<const dbl2*>(p));
+  return *reinterpret_cast<const dbl2*>(p);
+}
+template <bool NT>
+__device__ __forceinline__ void st2(double* p, dbl2 v) {
+  if (NT) __builtin_nontemporal_store(v, reinterpret_cast<dbl2*>(p));
+  else *reinterpret_cast<dbl2*>(p) = v;
+}
+
 // ---------------------------------------------------------------------------
-// ratio_kernel: entering column + pivot-column snapshot + min-ratio partials.
-// grid: NBr blocks, grid-stride over row pairs.
+// prime_kernel: pending entering column c (rule, or forced) + snapshot
+// F[slot] = T[:,c] + min-ratio partials.  grid: NBr blocks, grid-stride.
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(BLK) void ratio_kernel(const double* __restrict__ A, int64_t ld,
+__global__ __launch_bounds__(BLK) void prime_kernel(const double* __restrict__ A, int64_t ld,
                                                     int64_t m_local, int64_t row0, int64_t N,
                                                     const double* __restrict__ obj,
-                                                    double* __restrict__ F,
+                                                    double* __restrict__ F2,
                                                     const Key* __restrict__ enter_part, int nbn,
                                                     Key* __restrict__ ratio_part,
                                                     const int64_t* __restrict__ basis,
@@ -143,56 +192,44 @@ __global__ __launch_bounds__(BLK) void ratio_kernel(const double* __restrict__ A
   const int32_t rule = prm->rule;
   const double eps_piv = prm->eps_piv;
   const int64_t forced_c = st->forced_c;
+  const int slot = (int)(st->iters & 1);
   int64_t c;
   if (forced_c >= 0) {
     c = forced_c;
   } else {
-    if (st->iters >= prm->iter_limit) {
-      if (blockIdx.x == 0 && threadIdx.x == 0) st->status = ST_LIMIT;
-      return;
-    }
-    const Key e = reduce_keys(enter_part, nbn);
+    const KeyR e = reduce_keys(enter_part, nbn);
     if (e.row < 0) {
-      if (blockIdx.x == 0 && threadIdx.x == 0) st->status = ST_OPTIMAL;
+      if (blockIdx.x == 0 && threadIdx.x == 0) {
+        st->status = ST_OPTIMAL;
+        st->c_next = -1;
+      }
       return;
     }
     c = e.row;
   }
   if (blockIdx.x == 0 && threadIdx.x == 0) {
-    st->c = c;
-    st->zc = obj[c];
-    st->nz_count = 0;
+    st->c_next = c;
+    st->zc_next = obj[c];
+    st->count[slot] = 0;
+    st->n_ratio_part = gridDim.x;
   }
+  double* __restrict__ F = F2 + slot * ld;
   const double* __restrict__ colc = A + c * ld;
   const double* __restrict__ rhs = A + (N - 1) * ld;
-  Key k = key_none();
+  KeyR k = keyr_none();
   const bool forced = forced_c >= 0;
   for (int64_t i = ((int64_t)blockIdx.x * BLK + threadIdx.x) * 2; i < m_local;
        i += (int64_t)gridDim.x * BLK * 2) {
-    const double2 fv = *reinterpret_cast<const double2*>(colc + i);
-    const double2 bv = *reinterpret_cast<const double2*>(rhs + i);
-    *reinterpret_cast<double2*>(F + i) = fv;
+    const dbl2 fv = ld2<false>(colc + i);
+    const dbl2 bv = ld2<false>(rhs + i);
+    st2<false>(F + i, fv);
     if (!forced) {
-      if (fv.x > eps_piv) {
-        Key q;
-        q.v = bv.x / fv.x;
-        q.row = row0 + i;
-        q.t = (rule == RULE_BLAND) ? basis[row0 + i] : q.row;
-        q.pad = 0;
-        k = key_min(k, q);
-      }
-      if (i + 1 < m_local && fv.y > eps_piv) {
-        Key q;
-        q.v = bv.y / fv.y;
-        q.row = row0 + i + 1;
-        q.t = (rule == RULE_BLAND) ? basis[row0 + i + 1] : q.row;
-        q.pad = 0;
-        k = key_min(k, q);
-      }
+      ratio_candidate(k, fv.x, bv.x, row0 + i, basis, rule, eps_piv);
+      if (i + 1 < m_local) ratio_candidate(k, fv.y, bv.y, row0 + i + 1, basis, rule, eps_piv);
     }
   }
   k = block_min(k);
-  if (threadIdx.x == 0) ratio_part[blockIdx.x] = k;
+  if (threadIdx.x == 0) store_key(ratio_part + blockIdx.x, k);
 }
 
 // ---------------------------------------------------------------------------
@@ -204,7 +241,7 @@ __global__ __launch_bounds__(BLK) void ratio_kernel(const double* __restrict__ A
 //                         the other ranks write zeros.
 //   MODE_FINISH (sharded, after the all-reduce): objective, compaction,
 //                         entering partials, bookkeeping.
-//   MODE_INIT   entering partials only (after load / objective change).
+//   MODE_INIT   entering partials only (start of every host call).
 // ---------------------------------------------------------------------------
 constexpr int MODE_FUSED = 0;
 constexpr int MODE_PROW = 1;
@@ -215,7 +252,7 @@ template <int MODE>
 __global__ __launch_bounds__(BLK) void norm_kernel(const double* __restrict__ A, int64_t ld,
                                                    int64_t m_local, int64_t row0, int64_t N,
                                                    double* __restrict__ obj,
-                                                   const double* __restrict__ F,
+                                                   const double* __restrict__ F2,
                                                    double* __restrict__ P, int* __restrict__ list,
                                                    const Key* __restrict__ keys, int nkeys,
                                                    Key* __restrict__ enter_part,
@@ -228,12 +265,20 @@ __global__ __launch_bounds__(BLK) void norm_kernel(const double* __restrict__ A,
   const double eps_opt = prm->eps_opt;
   const int64_t n_enter = prm->n_enter;
   const bool skip = prm->skip_zero != 0;
+  const int64_t it = st->iters;
+  const int slot = (int)(it & 1);
+  const int64_t c = (MODE == MODE_INIT) ? -1 : st->c_next;
+  const int64_t forced_r = st->forced_r;
 
   int64_t r = -1;
   if (MODE == MODE_FUSED || MODE == MODE_PROW) {
-    r = st->forced_r;
+    if (c < 0 || (forced_r < 0 && it >= prm->iter_limit)) {
+      if (blockIdx.x == 0 && threadIdx.x == 0) st->status = (c < 0) ? ST_OPTIMAL : ST_LIMIT;
+      return;
+    }
+    r = forced_r;
     if (r < 0) {
-      const Key rk = reduce_keys(keys, nkeys);
+      const KeyR rk = reduce_keys(keys, MODE == MODE_FUSED ? st->n_ratio_part : nkeys);
       if (rk.row < 0) {
         if (blockIdx.x == 0 && threadIdx.x == 0) st->status = ST_UNBOUNDED;
         return;
@@ -241,24 +286,22 @@ __global__ __launch_bounds__(BLK) void norm_kernel(const double* __restrict__ A,
       r = rk.row;
     }
   }
+  const double* __restrict__ F = F2 + slot * ld;
 
   if (MODE == MODE_PROW) {
     const int64_t rl = r - row0;
-    if (j < N) {
-      double p = 0.0;
-      if (rl >= 0 && rl < m_local) p = A[j * ld + rl] / F[rl];
-      P[j] = p;
-    }
+    const bool owner = rl >= 0 && rl < m_local;
+    if (j < N) P[j] = owner ? A[j * ld + rl] / F[rl] : 0.0;
     if (blockIdx.x == 0 && threadIdx.x == 0) {
       st->r = r;
-      if (rl >= 0 && rl < m_local) st->piv = F[rl];
+      if (owner) st->piv = F[rl];
     }
     return;
   }
 
   bool nz = false;
-  Key ek = key_none();
-  const int64_t c = (MODE == MODE_INIT) ? -1 : st->c;
+  KeyR ek = keyr_none();
+  const double zc = st->zc_next;
   if (j < N) {
     double o = obj[j];
     if (MODE != MODE_INIT) {
@@ -273,15 +316,11 @@ __global__ __launch_bounds__(BLK) void norm_kernel(const double* __restrict__ A,
       if (j == c) {
         o = 0.0;
       } else if (nz) {
-        o = msub(o, st->zc, p);
+        o = msub(o, zc, p);
       }
       obj[j] = o;
     }
-    if (j < n_enter && o < -eps_opt) {
-      ek.v = (rule == RULE_BLAND) ? 0.0 : o;
-      ek.t = j;
-      ek.row = j;
-    }
+    if (j < n_enter && o < -eps_opt) kmin(ek, (rule == RULE_BLAND) ? 0.0 : o, j, j);
   }
 
   if (MODE != MODE_INIT) {
@@ -302,14 +341,14 @@ __global__ __launch_bounds__(BLK) void norm_kernel(const double* __restrict__ A,
         wbase[q] = s;
         s += wcount[q];
       }
-      bbase = s ? atomicAdd(&st->nz_count, s) : 0;
+      bbase = s ? atomicAdd(&st->count[slot], s) : 0;
     }
     __syncthreads();
     if (nz) list[bbase + wbase[w] + wpre] = (int)j;
   }
 
   ek = block_min(ek);
-  if (threadIdx.x == 0) enter_part[blockIdx.x] = ek;
+  if (threadIdx.x == 0) store_key(enter_part + blockIdx.x, ek);
 
   if (MODE != MODE_INIT && blockIdx.x == 0 && threadIdx.x == 0) {
     if (MODE == MODE_FUSED) {
@@ -318,100 +357,110 @@ __global__ __launch_bounds__(BLK) void norm_kernel(const double* __restrict__ A,
     } else {
       r = st->r;
     }
+    st->c = c;
+    st->zc = zc;
+    st->cur = slot;
     basis[r] = c;
-    const int64_t it = st->iters;
     if (it < st->hist_cap) {
       hist[2 * it] = r;
       hist[2 * it + 1] = c;
     }
-    st->iters = it + 1;
   }
 }
 
 // select_kernel (sharded): this rank's best leaving candidate -> sendkey.
-__global__ __launch_bounds__(BLK) void select_kernel(const Key* __restrict__ ratio_part, int nbr,
+__global__ __launch_bounds__(BLK) void select_kernel(const Key* __restrict__ ratio_part,
                                                      Key* __restrict__ sendkey, const State* st) {
-  const Key k = reduce_keys(ratio_part, nbr);
-  if (threadIdx.x == 0) {
-    if (st->status == ST_RUNNING) {
-      sendkey[0] = k;
-    } else {
-      sendkey[0] = key_none();
-    }
-  }
+  const bool live = st->status == ST_RUNNING && st->c_next >= 0;
+  const KeyR k = reduce_keys(ratio_part, live ? st->n_ratio_part : 0);
+  if (threadIdx.x == 0) store_key(sendkey, k);
 }
 
 // ---------------------------------------------------------------------------
-// elim_kernel: the rank-1 Gauss-Jordan update, HBM-bound.
-// grid = Rch * G blocks.  Block b owns row chunk (b % Rch) of RC = BLK*R rows
-// and column group (b / Rch) of the compacted column list.  Each thread keeps
-// its R pivot-column values F[i] in registers for the whole sweep and streams
-// R/2 16-B vectors per column, two columns in flight.  NT selects
-// non-temporal loads/stores for the once-touched stream.
+// elim_kernel: the rank-1 Gauss-Jordan update (HBM-bound) + the next pivot's
+// ratio test.  grid = rch * G blocks; block b owns row chunk (b % rch) of
+// RC = BLK*R rows and column group g = b / rch.  Each thread keeps its R values
+// of F in registers and streams R/2 16-B vectors per column, two columns in
+// flight.  Groups 1..G-1 (all groups if G == 1) share the compacted column
+// list, either in contiguous ranges or interleaved (ILV: at any moment the
+// active blocks sweep a contiguous window of the list).  Group 0 updates the
+// pending entering column c' and the RHS of its chunk, snapshots F' and writes
+// the chunk's ratio partial for the next pivot.  NTL / NTS select
+// non-temporal loads / stores for the once-touched stream.
 // ---------------------------------------------------------------------------
-typedef double dbl2 __attribute__((ext_vector_type(2)));
+template <int R, bool NTL, bool NTS>
+struct Elim {
+  static constexpr int V = R / 2;
 
-template <bool NT>
-__device__ __forceinline__ dbl2 ld2(const double* p) {
-  if (NT) return __builtin_nontemporal_load(reinterpret_cast<const dbl2*>(p));
-  return *reinterpret_cast<const dbl2*>(p);
-}
-template <bool NT>
-__device__ __forceinline__ void st2(double* p, dbl2 v) {
-  if (NT) __builtin_nontemporal_store(v, reinterpret_cast<dbl2*>(p));
-  else *reinterpret_cast<dbl2*>(p) = v;
-}
-
-template <int R, bool NT>
-__device__ __forceinline__ void elim_store(double* __restrict__ col, const dbl2 (&t)[R / 2],
-                                           const dbl2 (&f)[R / 2], const bool (&ok)[R / 2],
-                                           int64_t base, int64_t rl, double pj) {
+  __device__ static void load(const double* __restrict__ col, dbl2 (&t)[V],
+                              const bool (&ok)[V], int64_t base) {
 #pragma unroll
-  for (int v = 0; v < R / 2; ++v) {
-    const int64_t i = base + (int64_t)v * BLK * 2;
-    if (ok[v]) {
-      dbl2 o;
-      o.x = (i == rl) ? pj : msub(t[v].x, f[v].x, pj);
-      o.y = (i + 1 == rl) ? pj : msub(t[v].y, f[v].y, pj);
-      st2<NT>(col + i, o);
+    for (int v = 0; v < V; ++v)
+      if (ok[v]) t[v] = ld2<NTL>(col + base + (int64_t)v * BLK * 2);
+  }
+
+  __device__ static void update(double* __restrict__ col, const dbl2 (&t)[V],
+                                const dbl2 (&f)[V], const bool (&ok)[V], int64_t base,
+                                int64_t rl, double pj, dbl2 (&out)[V]) {
+#pragma unroll
+    for (int v = 0; v < V; ++v) {
+      const int64_t i = base + (int64_t)v * BLK * 2;
+      if (ok[v]) {
+        dbl2 o;
+        o.x = (i == rl) ? pj : msub(t[v].x, f[v].x, pj);
+        o.y = (i + 1 == rl) ? pj : msub(t[v].y, f[v].y, pj);
+        out[v] = o;
+        st2<NTS>(col + i, o);
+      }
     }
   }
-}
 
-template <int R, bool NT>
-__device__ __forceinline__ void elim_unit(double* __restrict__ col, const bool (&ok)[R / 2],
-                                          int64_t base, int64_t rl) {
+  __device__ static void unit(double* __restrict__ col, const bool (&ok)[V], int64_t base,
+                              int64_t rl) {
 #pragma unroll
-  for (int v = 0; v < R / 2; ++v) {
-    const int64_t i = base + (int64_t)v * BLK * 2;
-    if (ok[v]) {
-      dbl2 o;
-      o.x = (i == rl) ? 1.0 : 0.0;
-      o.y = (i + 1 == rl) ? 1.0 : 0.0;
-      st2<NT>(col + i, o);
+    for (int v = 0; v < V; ++v) {
+      const int64_t i = base + (int64_t)v * BLK * 2;
+      if (ok[v]) {
+        dbl2 o;
+        o.x = (i == rl) ? 1.0 : 0.0;
+        o.y = (i + 1 == rl) ? 1.0 : 0.0;
+        st2<NTS>(col + i, o);
+      }
     }
   }
-}
+};
 
-template <int R, bool NT>
-__global__ __launch_bounds__(BLK) void elim_kernel(double* __restrict__ A, int64_t ld,
-                                                   int64_t m_local, int64_t row0,
-                                                   const double* __restrict__ F,
-                                                   const double* __restrict__ P,
-                                                   const int* __restrict__ list, int rch, int G,
-                                                   State* st) {
+template <int R, bool NTL, bool NTS, bool ILV>
+__global__ __launch_bounds__(BLK) void elim_kernel(
+    double* __restrict__ A, int64_t ld, int64_t m_local, int64_t row0, int64_t N,
+    double* __restrict__ F2, const double* __restrict__ P, const int* __restrict__ list, int rch,
+    int G, const Key* __restrict__ enter_part, int nbn, Key* __restrict__ ratio_part,
+    const double* __restrict__ obj, const int64_t* __restrict__ basis,
+    const Params* __restrict__ prm, State* st) {
   static_assert(R % 2 == 0, "R must be even");
+  using E = Elim<R, NTL, NTS>;
   constexpr int V = R / 2;
   if (st->status != ST_RUNNING) return;
-  const int count = st->nz_count;
+  const int cur = st->cur;
+  const int count = st->count[cur];
   const int64_t c = st->c;
   const int64_t rl = st->r - row0;
-  if (blockIdx.x == 0 && threadIdx.x == 0) st->touched_total += count;
+  const int64_t rhs = N - 1;
+  const bool skip = prm->skip_zero != 0;
+  // the next pivot's entering column: every block must leave it (and the RHS)
+  // to group 0
+  const int64_t cn = reduce_keys(enter_part, nbn).row;
   const int chunk = blockIdx.x % rch;
   const int g = blockIdx.x / rch;
-  const int kb = (int)(((int64_t)g * count) / G);
-  const int ke = (int)(((int64_t)(g + 1) * count) / G);
-  if (kb >= ke) return;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    st->iters += 1;
+    st->count[cur ^ 1] = 0;
+    st->touched_total += count;
+    st->c_next = cn;
+    st->zc_next = cn >= 0 ? obj[cn] : 0.0;
+    st->n_ratio_part = rch;
+  }
+  const double* __restrict__ F = F2 + cur * ld;
 
   const int64_t base = (int64_t)chunk * BLK * R + threadIdx.x * 2;
   dbl2 f[V];
@@ -420,59 +469,83 @@ __global__ __launch_bounds__(BLK) void elim_kernel(double* __restrict__ A, int64
   for (int v = 0; v < V; ++v) {
     const int64_t i = base + (int64_t)v * BLK * 2;
     ok[v] = i < m_local;
-    f[v] = ok[v] ? *reinterpret_cast<const dbl2*>(F + i) : dbl2{0.0, 0.0};
+    f[v] = ok[v] ? ld2<false>(F + i) : dbl2{0.0, 0.0};
   }
 
-  int k = kb;
-  for (; k + 1 < ke; k += 2) {
-    const int j0 = list[k];
-    const int j1 = list[k + 1];
-    const double p0 = P[j0];
-    const double p1 = P[j1];
-    double* __restrict__ c0 = A + (int64_t)j0 * ld;
-    double* __restrict__ c1 = A + (int64_t)j1 * ld;
-    dbl2 t0[V], t1[V];
-#pragma unroll
-    for (int v = 0; v < V; ++v) {
-      const int64_t i = base + (int64_t)v * BLK * 2;
-      if (ok[v]) {
-        t0[v] = ld2<NT>(c0 + i);
-        t1[v] = ld2<NT>(c1 + i);
+  // ---- the compacted column list
+  const int LG = G > 1 ? G - 1 : 1;
+  const int lg = G > 1 ? g - 1 : 0;
+  if (lg >= 0) {
+    int k, ke, step;
+    if (ILV) {
+      k = lg;
+      ke = count;
+      step = LG;
+    } else {
+      k = (int)(((int64_t)lg * count) / LG);
+      ke = (int)(((int64_t)(lg + 1) * count) / LG);
+      step = 1;
+    }
+    dbl2 scratch[V];
+    for (;;) {
+      int j0 = -1, j1 = -1;
+      for (; k < ke && j0 < 0; k += step) {
+        const int j = list[k];
+        if (j != cn && j != rhs) j0 = j;
+      }
+      for (; k < ke && j1 < 0; k += step) {
+        const int j = list[k];
+        if (j != cn && j != rhs) j1 = j;
+      }
+      if (j0 < 0) break;
+      double* __restrict__ c0 = A + (int64_t)j0 * ld;
+      double* __restrict__ c1 = A + (int64_t)(j1 < 0 ? j0 : j1) * ld;
+      const double p0 = P[j0];
+      const double p1 = j1 < 0 ? 0.0 : P[j1];
+      dbl2 t0[V], t1[V];
+      if (j0 != c) E::load(c0, t0, ok, base);
+      if (j1 >= 0 && j1 != c) E::load(c1, t1, ok, base);
+      if (j0 == c) E::unit(c0, ok, base, rl);
+      else E::update(c0, t0, f, ok, base, rl, p0, scratch);
+      if (j1 >= 0) {
+        if (j1 == c) E::unit(c1, ok, base, rl);
+        else E::update(c1, t1, f, ok, base, rl, p1, scratch);
       }
     }
-    if (j0 == c) elim_unit<R, NT>(c0, ok, base, rl);
-    else elim_store<R, NT>(c0, t0, f, ok, base, rl, p0);
-    if (j1 == c) elim_unit<R, NT>(c1, ok, base, rl);
-    else elim_store<R, NT>(c1, t1, f, ok, base, rl, p1);
   }
-  if (k < ke) {
-    const int j0 = list[k];
-    const double p0 = P[j0];
-    double* __restrict__ c0 = A + (int64_t)j0 * ld;
-    if (j0 == c) {
-      elim_unit<R, NT>(c0, ok, base, rl);
-    } else {
-      dbl2 t0[V];
+
+  // ---- group 0: columns c' and RHS of this chunk + the next ratio test
+  if (g == 0) {
+    const int32_t rule = prm->rule;
+    const double eps_piv = prm->eps_piv;
+    dbl2 nb[V], nc[V];
+    {
+      double* __restrict__ col = A + rhs * ld;
+      const double pj = P[rhs];
+      E::load(col, nb, ok, base);
+      if (pj != 0.0 || !skip) E::update(col, nb, f, ok, base, rl, pj, nb);
+    }
+    KeyR k = keyr_none();
+    if (cn >= 0) {
+      double* __restrict__ col = A + cn * ld;
+      const double pj = P[cn];
+      E::load(col, nc, ok, base);
+      if (pj != 0.0 || !skip) E::update(col, nc, f, ok, base, rl, pj, nc);
+      double* __restrict__ Fn = F2 + (cur ^ 1) * ld;
 #pragma unroll
       for (int v = 0; v < V; ++v) {
         const int64_t i = base + (int64_t)v * BLK * 2;
-        if (ok[v]) t0[v] = ld2<NT>(c0 + i);
+        if (ok[v]) {
+          st2<false>(Fn + i, nc[v]);
+          ratio_candidate(k, nc[v].x, nb[v].x, row0 + i, basis, rule, eps_piv);
+          if (i + 1 < m_local)
+            ratio_candidate(k, nc[v].y, nb[v].y, row0 + i + 1, basis, rule, eps_piv);
+        }
       }
-      elim_store<R, NT>(c0, t0, f, ok, base, rl, p0);
     }
+    k = block_min(k);
+    if (threadIdx.x == 0) store_key(ratio_part + chunk, k);
   }
-}
-
-// Sum of nranks P buffers (in-process virtual ranks; RCCL does this across
-// processes).  Only one rank holds nonzeros, so the sum is exact.
-__global__ __launch_bounds__(BLK) void sum_rows_kernel(double* const* __restrict__ srcs,
-                                                       int nsrc, double* __restrict__ dst,
-                                                       int64_t n) {
-  const int64_t j = (int64_t)blockIdx.x * BLK + threadIdx.x;
-  if (j >= n) return;
-  double s = 0.0;
-  for (int q = 0; q < nsrc; ++q) s += srcs[q][j];
-  dst[j] = s;
 }
 
 }  // namespace spx

@@ -249,9 +249,10 @@ class DeviceTableau:
                     "spx_elim_timing")
         return float(ms.value), int(cnt.value), int(cols.value)
 
-    def set_elim_geometry(self, R: int = 0, target_wgs: int = 0) -> None:
-        self._check(self._lib.spx_set_elim_geometry(self._ctx, int(R), int(target_wgs)),
-                    "spx_set_elim_geometry")
-
-    def set_elim_nt(self, nt: bool) -> None:
-        self._check(self._lib.spx_set_elim_nt(self._ctx, 1 if nt else 0), "spx_set_elim_nt")
+    def set_elim_variant(self, R: int = 0, target_wgs: int = 0, nt_flags: int = 0,
+                         interleave: bool = False) -> None:
+        """Elimination-kernel tuning: rows per thread, grid target, non-temporal
+        flags (1 loads, 2 stores), interleaved column assignment."""
+        self._check(self._lib.spx_set_elim_variant(self._ctx, int(R), int(target_wgs),
+                                                   int(nt_flags), 1 if interleave else 0),
+                    "spx_set_elim_variant")

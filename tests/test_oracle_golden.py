@@ -125,3 +125,18 @@ def test_generated_lps_oracle_vs_highs(e):
     assert T[-1, -1] == e["oracle_objective"]
     hz = e["highs_objective"]
     assert abs(T[-1, -1] - hz) <= 1e-9 * max(1.0, abs(hz))
+
+
+@pytest.mark.parametrize("kind,m,n,seed,rule", [("dense", 64, 96, 7, "dantzig"),
+                                                 ("dense", 200, 300, 11, "dantzig"),
+                                                 ("degenerate", 64, 64, 5, "bland")])
+@pytest.mark.parametrize("skip", [True, False])
+def test_c_oracle_bit_identical_to_numpy_oracle(kind, m, n, seed, rule, skip):
+    from oracle import c_oracle as C
+    from simplex_amd import synth
+    T, b = synth.full_tableau(kind, m, n, seed)
+    T2, b2 = T.copy(), b.copy()
+    st, h = O.solve_tableau(T, b, rule=rule, max_iters=100000, skip_zero=skip)
+    st2, h2 = C.solve(T2, b2, rule=rule, skip_zero=skip)
+    assert st == st2 and h == h2 and np.array_equal(b, b2)
+    assert T.tobytes() == T2.tobytes()
