@@ -46,9 +46,10 @@ def parse():
     ap.add_argument("--ilv", type=int, default=-1, help="elim interleaved columns (-1: default)")
     ap.add_argument("--R", type=int, default=0, help="elim rows per thread (0: auto)")
     ap.add_argument("--wgs", type=int, default=0, help="elim grid target (0: auto)")
-    ap.add_argument("--graph", type=int, default=-1,
-                    help="1: time hipGraph replays (elim events in a separate window); "
-                         "0: direct launches with per-elim events; -1: auto (N>1 -> 1)")
+    ap.add_argument("--graph", type=int, default=1,
+                    help="1: the timed region replays one hipGraph with an event pair "
+                         "captured around every elimination; 0: direct launches + events")
+    ap.add_argument("--ld-pad", type=int, default=-1, help="column padding (doubles)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0,
                     help="budget of the CPU-baseline sample (0 disables)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles",
@@ -105,7 +106,7 @@ def main():
     world, rank, local = dist_env()
     if args.gpus != world and world > 1:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE {world}")
-    use_graph = (world > 1) if args.graph < 0 else bool(args.graph)
+    use_graph = bool(args.graph)
 
     import torch  # device discovery / distributed plumbing only
     import torch.distributed as tdist
@@ -122,13 +123,15 @@ def main():
         eng = ShardedTableau(local, rank, world, uid)
     else:
         eng = DeviceTableau(0)
+    if args.ld_pad >= 0:
+        eng.set_ld_pad(args.ld_pad)
     row0, row1 = row_partition(m, world, rank)
     Tf, obj, basis = synth.tableau_rows("dense", m, n, args.seed, row0, row1, order="F")
     eng.load_rows(Tf, obj, basis, m, row0)
     del Tf
     if args.nt >= 0 or args.ilv >= 0 or args.R or args.wgs:
         eng.set_elim_variant(args.R, args.wgs, max(args.nt, 0), args.ilv > 0)
-    opts = dict(rule=args.rule, skip_zero_cols=not args.dense, use_graph=True, chunk=32)
+    opts = dict(rule=args.rule, skip_zero_cols=not args.dense, use_graph=use_graph, chunk=32)
 
     def barrier():
         if world > 1:
@@ -140,7 +143,7 @@ def main():
     barrier()
     eng.sync()
     t0 = time.perf_counter()
-    eng.run_pivots(args.steps, time_elim=not use_graph, **opts)
+    eng.run_pivots(args.steps, time_elim=True, **opts)
     eng.sync()
     t1 = time.perf_counter()
     barrier()
@@ -153,12 +156,9 @@ def main():
     if status != 4 or iters != args.warmup + args.steps:
         raise SystemExit(f"pivot loop ended early: status {status}, iters {iters}")
     ms_tot, launches, touched = eng.elim_timing(reset=True)
-    window = "timed region (per-launch HIP events on the engine stream)"
-    if use_graph or launches == 0:
-        eng.run_pivots(64, time_elim=True, **opts)
-        eng.sync()
-        ms_tot, launches, touched = eng.elim_timing(reset=True)
-        window = "64-pivot event window right after the graph-timed region"
+    window = ("timed region: HIP event nodes captured around every elimination in the "
+              "replayed hipGraph, on the engine stream" if use_graph else
+              "timed region: HIP events around every elimination launch, engine stream")
     avg_ms = ms_tot / launches
     m_local = row1 - row0
     N = n + m + 1
@@ -201,6 +201,7 @@ def main():
                        "m": m, "n": n, "tableau": [m + 1, N], "rule": args.rule,
                        "elimination": "dense sweep" if args.dense else "skip p[j]==0 columns",
                        "timing": "hipGraph replay" if use_graph else "direct launches",
+                       "ld_pad": args.ld_pad,
                        "parallelism": f"row-shard x{world}" if world > 1 else "single GPU"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBPS,

@@ -107,12 +107,16 @@ struct spx_ctx {
   int nbn = 1, nbr = 1, rch = 1, G = 1, R = 8;
   int elim_nt = 0;         // bit 0: non-temporal loads, bit 1: non-temporal stores
   int elim_ilv = 0;        // interleaved column assignment
+  int ld_pad = 0;          // extra doubles per column (breaks power-of-two strides)
   int tune_R = 0;          // 0: automatic
   int tune_wgs = 0;        // 0: automatic (2048)
 
   // graph cache
   hipGraphExec_t gexec = nullptr;
   int gchunk = 0;
+  hipGraphExec_t texec = nullptr;   // event-timed graph of the last spx_run_pivots
+  int64_t tpivots = 0;
+  size_t tev0 = 0;                  // first event index the timed graph records
 
   // elimination timing
   std::vector<std::pair<hipEvent_t, hipEvent_t>> ev;
@@ -154,10 +158,16 @@ void dfree(T*& p) {
   p = nullptr;
 }
 
-int free_buffers(spx_ctx* ctx) {
+void drop_graphs(spx_ctx* ctx) {
   if (ctx->gexec) (void)hipGraphExecDestroy(ctx->gexec);
-  ctx->gexec = nullptr;
+  if (ctx->texec) (void)hipGraphExecDestroy(ctx->texec);
+  ctx->gexec = ctx->texec = nullptr;
   ctx->gchunk = 0;
+  ctx->tpivots = 0;
+}
+
+int free_buffers(spx_ctx* ctx) {
+  drop_graphs(ctx);
   dfree(ctx->A);
   dfree(ctx->obj);
   dfree(ctx->F);
@@ -318,9 +328,10 @@ int enqueue_pivot(spx_ctx* ctx, bool time_elim) {
       ctx->ev.emplace_back(a, b);
     }
     auto& e = ctx->ev[ctx->ev_used++];
-    HIPC(hipEventRecord(e.first, ctx->stream));
+    // external event nodes when captured (hipGraph), plain records otherwise
+    HIPC(hipEventRecordWithFlags(e.first, ctx->stream, hipEventRecordExternal));
     launch_elim(ctx);
-    HIPC(hipEventRecord(e.second, ctx->stream));
+    HIPC(hipEventRecordWithFlags(e.second, ctx->stream, hipEventRecordExternal));
   } else {
     launch_elim(ctx);
   }
@@ -419,7 +430,7 @@ int alloc_common(spx_ctx* ctx, int64_t m_local, int64_t N, int64_t m_global, int
   ctx->m_global = m_global;
   ctx->row0 = row0;
   ctx->N = N;
-  ctx->ld = std::max<int64_t>(64, round_up(m_local, 64));
+  ctx->ld = std::max<int64_t>(64, round_up(m_local, 64)) + ctx->ld_pad;
   choose_geometry(ctx);
   ctx->hist_cap = 1 << 20;
   HIPC(hipSetDevice(ctx->device));
@@ -808,7 +819,37 @@ int spx_run_pivots(spx_ctx* ctx, const spx_opts* opts, int64_t npivots, int time
   const spx_opts* o = opts ? opts : &d;
   int rc = begin_call(ctx, o);
   if (rc) return rc;
-  if (!time_elim && o->use_graph && !ctx->loop) {
+  const bool graph = o->use_graph && !ctx->loop;
+  if (time_elim && graph) {
+    // one graph of exactly npivots pivots with an event pair around every
+    // elimination; instantiated before it is launched (outside any timing)
+    if (ctx->texec && (ctx->tpivots != npivots || ctx->tev0 != ctx->ev_used)) {
+      (void)hipGraphExecDestroy(ctx->texec);
+      ctx->texec = nullptr;
+    }
+    if (!ctx->texec) {
+      const size_t ev0 = ctx->ev_used;
+      hipGraph_t g = nullptr;
+      HIPC(hipStreamBeginCapture(ctx->stream, hipStreamCaptureModeThreadLocal));
+      for (int64_t i = 0; i < npivots && rc == SPX_OK; ++i) rc = enqueue_pivot(ctx, true);
+      hipError_t e = hipStreamEndCapture(ctx->stream, &g);
+      if (rc == SPX_OK && e == hipSuccess) e = hipGraphInstantiate(&ctx->texec, g, nullptr, nullptr, 0);
+      if (g) (void)hipGraphDestroy(g);
+      ctx->ev_used = ev0;  // the launch below re-records the same events
+      if (rc) return rc;
+      if (e != hipSuccess) {
+        ctx->texec = nullptr;
+        ctx->err = std::string("timed graph: ") + hipGetErrorString(e);
+        return SPX_E_HIP;
+      }
+      ctx->tpivots = npivots;
+      ctx->tev0 = ev0;
+    }
+    ctx->ev_used += (size_t)npivots;
+    HIPC(hipGraphLaunch(ctx->texec, ctx->stream));
+    return SPX_OK;
+  }
+  if (!time_elim && graph) {
     const int chunk = o->chunk > 0 ? o->chunk : 32;
     if ((rc = build_graph(ctx, chunk))) return rc;
     int64_t left = npivots;
@@ -881,9 +922,15 @@ int spx_set_elim_variant(spx_ctx* ctx, int R, int target_wgs, int nt_flags, int 
       HIPC(hipMalloc(&ctx->ratio_part, sizeof(Key) * std::max(ctx->nbr, ctx->rch)));
     }
   }
-  if (ctx->gexec) (void)hipGraphExecDestroy(ctx->gexec);
-  ctx->gexec = nullptr;
-  ctx->gchunk = 0;
+  drop_graphs(ctx);
+  return SPX_OK;
+}
+
+// Layout knob: extra doubles per column; takes effect at the next load.
+int spx_set_ld_pad(spx_ctx* ctx, int pad) {
+  if (!ctx) return SPX_E_ARG;
+  CHECK_ARG(pad >= 0 && pad % 2 == 0 && pad <= 4096, "ld pad must be even, 0..4096");
+  ctx->ld_pad = pad;
   return SPX_OK;
 }
 

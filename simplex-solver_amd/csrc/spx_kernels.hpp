@@ -165,6 +165,14 @@ __device__ __forceinline__ void ratio_candidate(KeyR& k, double fv, double bv, i
 
 typedef double dbl2 __attribute__((ext_vector_type(2)));
 
+// v_readlane of a double held per lane (lane index wave-uniform).
+__device__ __forceinline__ double rdlane(double v, int lane) {
+  const int64_t b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffff), lane);
+  const int hi = __builtin_amdgcn_readlane((int)(b >> 32), lane);
+  return __longlong_as_double(((int64_t)hi << 32) | (uint32_t)lo);
+}
+
 template <bool NT>
 __device__ __forceinline__ dbl2 ld2(const double* p) {
   if (NT) return __builtin_nontemporal_load(reinterpret_cast<const dbl2*>(p));
@@ -472,44 +480,54 @@ __global__ __launch_bounds__(BLK) void elim_kernel(
     f[v] = ok[v] ? ld2<false>(F + i) : dbl2{0.0, 0.0};
   }
 
-  // ---- the compacted column list
+  // ---- the compacted column list, read 64 entries at a time into lanes (one
+  // vector load of list[] and one gather of P[] per window), then walked with
+  // v_readlane so the stream loop issues no dependent scalar loads
   const int LG = G > 1 ? G - 1 : 1;
   const int lg = G > 1 ? g - 1 : 0;
   if (lg >= 0) {
-    int k, ke, step;
+    int kb, ke, step;
     if (ILV) {
-      k = lg;
+      kb = lg;
       ke = count;
       step = LG;
     } else {
-      k = (int)(((int64_t)lg * count) / LG);
+      kb = (int)(((int64_t)lg * count) / LG);
       ke = (int)(((int64_t)(lg + 1) * count) / LG);
       step = 1;
     }
+    const int lane = threadIdx.x & 63;
     dbl2 scratch[V];
-    for (;;) {
-      int j0 = -1, j1 = -1;
-      for (; k < ke && j0 < 0; k += step) {
-        const int j = list[k];
-        if (j != cn && j != rhs) j0 = j;
+    for (int w0 = kb; w0 < ke; w0 += 64 * step) {
+      const int kk = w0 + lane * step;
+      int jl = -1;
+      double pl = 0.0;
+      if (kk < ke) {
+        jl = list[kk];
+        if (jl == cn || jl == rhs) jl = -1;
+        else pl = P[jl];
       }
-      for (; k < ke && j1 < 0; k += step) {
-        const int j = list[k];
-        if (j != cn && j != rhs) j1 = j;
-      }
-      if (j0 < 0) break;
-      double* __restrict__ c0 = A + (int64_t)j0 * ld;
-      double* __restrict__ c1 = A + (int64_t)(j1 < 0 ? j0 : j1) * ld;
-      const double p0 = P[j0];
-      const double p1 = j1 < 0 ? 0.0 : P[j1];
-      dbl2 t0[V], t1[V];
-      if (j0 != c) E::load(c0, t0, ok, base);
-      if (j1 >= 0 && j1 != c) E::load(c1, t1, ok, base);
-      if (j0 == c) E::unit(c0, ok, base, rl);
-      else E::update(c0, t0, f, ok, base, rl, p0, scratch);
-      if (j1 >= 0) {
-        if (j1 == c) E::unit(c1, ok, base, rl);
-        else E::update(c1, t1, f, ok, base, rl, p1, scratch);
+      const int nwin = min(64, (ke - w0 + step - 1) / step);
+      int q = 0;
+      for (;;) {
+        int j0 = -1, j1 = -1;
+        double p0 = 0.0, p1 = 0.0;
+        for (; q < nwin && j0 < 0; ++q) j0 = __builtin_amdgcn_readlane(jl, q);
+        if (j0 >= 0) p0 = rdlane(pl, q - 1);
+        for (; q < nwin && j1 < 0; ++q) j1 = __builtin_amdgcn_readlane(jl, q);
+        if (j1 >= 0) p1 = rdlane(pl, q - 1);
+        if (j0 < 0) break;
+        double* __restrict__ c0 = A + (int64_t)j0 * ld;
+        double* __restrict__ c1 = A + (int64_t)(j1 < 0 ? j0 : j1) * ld;
+        dbl2 t0[V], t1[V];
+        if (j0 != c) E::load(c0, t0, ok, base);
+        if (j1 >= 0 && j1 != c) E::load(c1, t1, ok, base);
+        if (j0 == c) E::unit(c0, ok, base, rl);
+        else E::update(c0, t0, f, ok, base, rl, p0, scratch);
+        if (j1 >= 0) {
+          if (j1 == c) E::unit(c1, ok, base, rl);
+          else E::update(c1, t1, f, ok, base, rl, p1, scratch);
+        }
       }
     }
   }

@@ -249,6 +249,10 @@ class DeviceTableau:
                     "spx_elim_timing")
         return float(ms.value), int(cnt.value), int(cols.value)
 
+    def set_ld_pad(self, pad: int) -> None:
+        """Extra doubles per stored column, applied at the next load."""
+        self._check(self._lib.spx_set_ld_pad(self._ctx, int(pad)), "spx_set_ld_pad")
+
     def set_elim_variant(self, R: int = 0, target_wgs: int = 0, nt_flags: int = 0,
                          interleave: bool = False) -> None:
         """Elimination-kernel tuning: rows per thread, grid target, non-temporal

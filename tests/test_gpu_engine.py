@@ -362,3 +362,44 @@ def test_sharded_virtual_ranks_bit_exact(world, kind, m, n, rule):
         assert np.array_equal(Tl[:-1], T[r0:r1])
         assert np.array_equal(Tl[-1], T[-1])
         assert np.array_equal(b, basis)
+
+
+def test_run_pivots_timed_graph_matches_untimed(eng_cls):
+    """bench.py's timed region (one hipGraph with event nodes around every
+    elimination) computes exactly what the plain pivot loop computes."""
+    from simplex_amd import synth
+    T, basis = synth.full_tableau("dense", 300, 500, 21)
+    outs = []
+    for kw in (dict(time_elim=True, use_graph=True), dict(time_elim=True, use_graph=False),
+               dict(time_elim=False, use_graph=True)):
+        with eng_cls(0) as e:
+            e.set_ld_pad(64)
+            e.load(T, basis)
+            e.run_pivots(5)
+            e.sync()
+            e.elim_timing(reset=True)
+            e.run_pivots(40, **kw)
+            e.sync()
+            ms, cnt, cols = e.elim_timing(reset=True)
+            if kw["time_elim"]:
+                assert cnt == 40 and ms > 0 and cols > 0
+            outs.append((e.history().tolist(), e.tableau()))
+    for h, t in outs[1:]:
+        assert h == outs[0][0] and np.array_equal(t, outs[0][1])
+    ref, rb = T.copy(), basis.copy()
+    st, hist = O.solve_tableau(ref, rb, max_iters=45)
+    assert [tuple(x) for x in outs[0][0]] == hist and np.array_equal(outs[0][1], ref)
+
+
+@pytest.mark.parametrize("pad", [0, 2, 64, 130])
+def test_ld_padding_is_transparent(eng_cls, pad):
+    from simplex_amd import synth
+    T, basis = synth.full_tableau("dense", 257, 300, 4)
+    ref, rb = T.copy(), basis.copy()
+    st, hist = O.solve_tableau(ref, rb)
+    with eng_cls(0) as e:
+        e.set_ld_pad(pad)
+        e.load(T, basis)
+        r = e.solve()
+        assert [tuple(x) for x in e.history().tolist()] == hist
+        assert np.array_equal(e.tableau(), ref) and r.objective == ref[-1, -1]
