@@ -161,7 +161,7 @@ int spx_elim_timing(spx_ctx* ctx, double* total_ms, int64_t* count, int64_t* tou
  * interleaved column assignment (1) instead of contiguous column ranges (0). */
 int spx_set_elim_variant(spx_ctx* ctx, int R, int target_wgs, int nt_flags, int interleave);
 /* Layout knob: extra doubles of padding per stored column (even, 0..4096);
- * applies to the next spx_load / spx_load_rows. */
+  * applies to the next spx_load / spx_load_rows; -1 = automatic. */
 int spx_set_ld_pad(spx_ctx* ctx, int pad);
 
 #ifdef __cplusplus

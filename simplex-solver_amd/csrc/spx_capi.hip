@@ -106,8 +106,8 @@ struct spx_ctx {
   // launch geometry
   int nbn = 1, nbr = 1, rch = 1, G = 1, R = 8;
   int elim_nt = 0;         // bit 0: non-temporal loads, bit 1: non-temporal stores
-  int elim_ilv = 0;        // interleaved column assignment
-  int ld_pad = 0;          // extra doubles per column (breaks power-of-two strides)
+  int elim_ilv = 1;        // interleaved column assignment
+  int ld_pad = -1;         // extra doubles per column (-1: auto, 256 for big shards)
   int tune_R = 0;          // 0: automatic
   int tune_wgs = 0;        // 0: automatic (2048)
 
@@ -189,11 +189,13 @@ int64_t round_up(int64_t x, int64_t a) { return (x + a - 1) / a * a; }
 // Elimination geometry: rows per thread R, row chunks rch, column groups G.
 void choose_geometry(spx_ctx* ctx) {
   const int64_t m = ctx->m_local;
-  ctx->R = (m >= 4096) ? 8 : (m >= 1024 ? 4 : 2);
+  ctx->R = (m >= 1024) ? 4 : 2;
   if (ctx->tune_R == 2 || ctx->tune_R == 4 || ctx->tune_R == 8) ctx->R = ctx->tune_R;
   const int64_t rc = (int64_t)BLK * ctx->R;
   ctx->rch = (int)std::max<int64_t>(1, (m + rc - 1) / rc);
-  const int target = ctx->tune_wgs > 0 ? ctx->tune_wgs : 2048;  // 256 CUs x 8 workgroups
+  // measured on config 3 (tools/tune_elim.py): ~5 workgroups per CU streaming
+  // interleaved column windows beats a full 8-per-CU grid
+  const int target = ctx->tune_wgs > 0 ? ctx->tune_wgs : 1280;
   ctx->G = std::max(1, target / ctx->rch);
   ctx->G = (int)std::min<int64_t>(ctx->G, std::max<int64_t>(1, ctx->N));
   ctx->nbn = (int)std::max<int64_t>(1, (ctx->N + BLK - 1) / BLK);
@@ -307,6 +309,27 @@ int comm_allreduce_p(spx_ctx* ctx) {
   return SPX_OK;
 }
 
+// Record a timing event on the stream; while the stream is being captured,
+// insert an event-record node into the capture graph in stream order instead.
+int record_event(spx_ctx* ctx, hipEvent_t ev) {
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  HIPC(hipStreamIsCapturing(ctx->stream, &cs));
+  if (cs != hipStreamCaptureStatusActive) {
+    HIPC(hipEventRecord(ev, ctx->stream));
+    return SPX_OK;
+  }
+  unsigned long long id = 0;
+  hipGraph_t g = nullptr;
+  const hipGraphNode_t* deps = nullptr;
+  size_t ndeps = 0;
+  HIPC(hipStreamGetCaptureInfo_v2(ctx->stream, &cs, &id, &g, &deps, &ndeps));
+  hipGraphNode_t node;
+  HIPC(hipGraphAddEventRecordNode(&node, g, deps, ndeps, ev));
+  HIPC(hipStreamUpdateCaptureDependencies(ctx->stream, &node, 1,
+                                          hipStreamSetCaptureDependencies));
+  return SPX_OK;
+}
+
 // Enqueue one pivot (all launches on ctx->stream; no host synchronisation).
 int enqueue_pivot(spx_ctx* ctx, bool time_elim) {
   if (!ctx->sharded) {
@@ -328,10 +351,10 @@ int enqueue_pivot(spx_ctx* ctx, bool time_elim) {
       ctx->ev.emplace_back(a, b);
     }
     auto& e = ctx->ev[ctx->ev_used++];
-    // external event nodes when captured (hipGraph), plain records otherwise
-    HIPC(hipEventRecordWithFlags(e.first, ctx->stream, hipEventRecordExternal));
+    int rc = record_event(ctx, e.first);
+    if (rc) return rc;
     launch_elim(ctx);
-    HIPC(hipEventRecordWithFlags(e.second, ctx->stream, hipEventRecordExternal));
+    if ((rc = record_event(ctx, e.second))) return rc;
   } else {
     launch_elim(ctx);
   }
@@ -377,6 +400,7 @@ int begin_call(spx_ctx* ctx, const spx_opts* o, int64_t fc = -1, int64_t fr = -1
     ctx->err = "no tableau loaded";
     return SPX_E_STATE;
   }
+  (void)hipGetLastError();  // drop a stale error of an unrelated earlier call
   int rc = pull_state(ctx);
   if (rc) return rc;
   if ((rc = write_params(ctx, o))) return rc;
@@ -430,7 +454,8 @@ int alloc_common(spx_ctx* ctx, int64_t m_local, int64_t N, int64_t m_global, int
   ctx->m_global = m_global;
   ctx->row0 = row0;
   ctx->N = N;
-  ctx->ld = std::max<int64_t>(64, round_up(m_local, 64)) + ctx->ld_pad;
+  const int pad = ctx->ld_pad >= 0 ? ctx->ld_pad : (m_local >= 2048 ? 256 : 0);
+  ctx->ld = std::max<int64_t>(64, round_up(m_local, 64)) + pad;
   choose_geometry(ctx);
   ctx->hist_cap = 1 << 20;
   HIPC(hipSetDevice(ctx->device));
@@ -929,7 +954,8 @@ int spx_set_elim_variant(spx_ctx* ctx, int R, int target_wgs, int nt_flags, int 
 // Layout knob: extra doubles per column; takes effect at the next load.
 int spx_set_ld_pad(spx_ctx* ctx, int pad) {
   if (!ctx) return SPX_E_ARG;
-  CHECK_ARG(pad >= 0 && pad % 2 == 0 && pad <= 4096, "ld pad must be even, 0..4096");
+  CHECK_ARG(pad == -1 || (pad >= 0 && pad % 2 == 0 && pad <= 4096),
+            "ld pad must be -1 (auto) or even, 0..4096");
   ctx->ld_pad = pad;
   return SPX_OK;
 }

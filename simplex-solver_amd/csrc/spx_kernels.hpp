@@ -455,21 +455,13 @@ __global__ __launch_bounds__(BLK) void elim_kernel(
   const int64_t rl = st->r - row0;
   const int64_t rhs = N - 1;
   const bool skip = prm->skip_zero != 0;
-  // the next pivot's entering column: every block must leave it (and the RHS)
-  // to group 0
-  const int64_t cn = reduce_keys(enter_part, nbn).row;
   const int chunk = blockIdx.x % rch;
   const int g = blockIdx.x / rch;
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
-    st->iters += 1;
-    st->count[cur ^ 1] = 0;
-    st->touched_total += count;
-    st->c_next = cn;
-    st->zc_next = cn >= 0 ? obj[cn] : 0.0;
-    st->n_ratio_part = rch;
-  }
   const double* __restrict__ F = F2 + cur * ld;
 
+  // Issue the loads that do not depend on c' first (pivot-column values of
+  // this chunk, the first 64-entry window of this group's column list and the
+  // matching p values), so they are in flight during the c' reduction.
   const int64_t base = (int64_t)chunk * BLK * R + threadIdx.x * 2;
   dbl2 f[V];
   bool ok[V];
@@ -479,14 +471,10 @@ __global__ __launch_bounds__(BLK) void elim_kernel(
     ok[v] = i < m_local;
     f[v] = ok[v] ? ld2<false>(F + i) : dbl2{0.0, 0.0};
   }
-
-  // ---- the compacted column list, read 64 entries at a time into lanes (one
-  // vector load of list[] and one gather of P[] per window), then walked with
-  // v_readlane so the stream loop issues no dependent scalar loads
   const int LG = G > 1 ? G - 1 : 1;
   const int lg = G > 1 ? g - 1 : 0;
+  int kb = 0, ke = 0, step = 1;
   if (lg >= 0) {
-    int kb, ke, step;
     if (ILV) {
       kb = lg;
       ke = count;
@@ -494,28 +482,63 @@ __global__ __launch_bounds__(BLK) void elim_kernel(
     } else {
       kb = (int)(((int64_t)lg * count) / LG);
       ke = (int)(((int64_t)(lg + 1) * count) / LG);
-      step = 1;
     }
-    const int lane = threadIdx.x & 63;
+  }
+  const int lane = threadIdx.x & 63;
+  int jl = -1;
+  double pl = 0.0;
+  {
+    const int kk = kb + lane * step;
+    if (kk < ke) {
+      jl = list[kk];
+      pl = P[jl];
+    }
+  }
+
+  // the next pivot's entering column: every block must leave it (and the RHS)
+  // to group 0
+  const int64_t cn = reduce_keys(enter_part, nbn).row;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    st->iters += 1;
+    st->count[cur ^ 1] = 0;
+    st->touched_total += count;
+    st->c_next = cn;
+    st->zc_next = cn >= 0 ? obj[cn] : 0.0;
+    st->n_ratio_part = rch;
+  }
+
+  // ---- the compacted column list, 64 entries at a time held in lanes and
+  // walked with v_readlane (no dependent scalar loads in the stream loop)
+  if (lg >= 0) {
     dbl2 scratch[V];
     for (int w0 = kb; w0 < ke; w0 += 64 * step) {
-      const int kk = w0 + lane * step;
-      int jl = -1;
-      double pl = 0.0;
-      if (kk < ke) {
-        jl = list[kk];
-        if (jl == cn || jl == rhs) jl = -1;
-        else pl = P[jl];
+      if (w0 != kb) {
+        const int kk = w0 + lane * step;
+        jl = -1;
+        if (kk < ke) {
+          jl = list[kk];
+          pl = P[jl];
+        }
       }
       const int nwin = min(64, (ke - w0 + step - 1) / step);
       int q = 0;
       for (;;) {
         int j0 = -1, j1 = -1;
         double p0 = 0.0, p1 = 0.0;
-        for (; q < nwin && j0 < 0; ++q) j0 = __builtin_amdgcn_readlane(jl, q);
-        if (j0 >= 0) p0 = rdlane(pl, q - 1);
-        for (; q < nwin && j1 < 0; ++q) j1 = __builtin_amdgcn_readlane(jl, q);
-        if (j1 >= 0) p1 = rdlane(pl, q - 1);
+        for (; q < nwin && j0 < 0; ++q) {
+          const int j = __builtin_amdgcn_readlane(jl, q);
+          if (j != cn && j != rhs) {
+            j0 = j;
+            p0 = rdlane(pl, q);
+          }
+        }
+        for (; q < nwin && j1 < 0; ++q) {
+          const int j = __builtin_amdgcn_readlane(jl, q);
+          if (j != cn && j != rhs) {
+            j1 = j;
+            p1 = rdlane(pl, q);
+          }
+        }
         if (j0 < 0) break;
         double* __restrict__ c0 = A + (int64_t)j0 * ld;
         double* __restrict__ c1 = A + (int64_t)(j1 < 0 ? j0 : j1) * ld;

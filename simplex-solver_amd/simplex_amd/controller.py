@@ -16,12 +16,14 @@ visualisation HTML is the static tableau HTML of its Plan B (:190-200).
 """
 from __future__ import annotations
 
+import os
 import traceback
 from typing import Any, Dict, List, Tuple
 
 import numpy as np
 from scipy.optimize import linprog  # answer path + mock seam (:9, :78-85)
 
+from .linprog import linprog as gpu_linprog
 from .storage import StorageService
 from .simple_simplex import (add_constraint, add_objective, create_tableau,
                              optimize_json_format)
@@ -34,7 +36,13 @@ TABLE_OPEN = ('<table class="table table-bordered table-striped" style="border:1
 
 
 class SolverController:
-    def __init__(self, problem_data_wrapper: dict):
+    def __init__(self, problem_data_wrapper: dict, answer_engine: str | None = None):
+        """answer_engine: "highs" (default, the reference's scipy/HiGHS call
+        through the module-level ``linprog`` seam) or "gpu" (simplex_amd.linprog,
+        the same two-phase GPU engine that produces the tables)."""
+        self.answer_engine = (answer_engine or os.environ.get("SPX_ANSWER_ENGINE", "highs")).lower()
+        if self.answer_engine not in ("highs", "gpu"):
+            raise ValueError(f"unknown answer engine {self.answer_engine!r}")
         self.storage = StorageService()
         definition = (problem_data_wrapper or {}).get("problema_definicion", {})
         self.objective_data = definition.get("funcion_objetivo")
@@ -54,8 +62,9 @@ class SolverController:
             c, A_ub, b_ub, A_eq, b_eq, bounds = self._prepare_model_for_scipy(
                 self.objective_data, self.constraints_data, self.variables)
             print("Ejecutando solver principal (Scipy)...")
-            result = linprog(c, A_ub=A_ub, b_ub=b_ub, A_eq=A_eq, b_eq=b_eq, bounds=bounds,
-                             method="highs-ds", options=dict(SOLVER_OPTIONS))
+            solve = linprog if self.answer_engine == "highs" else gpu_linprog
+            result = solve(c, A_ub=A_ub, b_ub=b_ub, A_eq=A_eq, b_eq=b_eq, bounds=bounds,
+                           method="highs-ds", options=dict(SOLVER_OPTIONS))
             if result.success:
                 print("Generando visualización (tablas del motor de pivoteo)...")
                 html, tables = self._generate_visualization_html_and_tables()

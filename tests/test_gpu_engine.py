@@ -403,3 +403,90 @@ def test_ld_padding_is_transparent(eng_cls, pad):
         r = e.solve()
         assert [tuple(x) for x in e.history().tolist()] == hist
         assert np.array_equal(e.tableau(), ref) and r.objective == ref[-1, -1]
+
+
+# ----------------------------------------------------------- linprog adapter, controller
+LP_CASES = [
+    dict(c=[-3, -5], A_ub=[[1, 0], [0, 2], [3, 2]], b_ub=[4, 12, 18]),
+    dict(c=[50, 80], A_ub=[[-4, -1], [-1, -6], [-4, -6]], b_ub=[-4, -6, -12]),
+    dict(c=[-1, -1], A_ub=[[1, 1], [-1, -1], [2, 1]], b_ub=[10, -10, 15], A_eq=[[1, 1]],
+         b_eq=[10]),
+    dict(c=[-1], A_ub=[[1], [-1]], b_ub=[5, -10]),                       # infeasible
+    dict(c=[-1, -1], A_ub=[[1, -1]], b_ub=[1]),                           # unbounded
+    dict(c=[1, -2, 3], A_ub=[[1, 1, 1], [1, -1, 0]], b_ub=[7, 2], A_eq=[[0, 1, 1]], b_eq=[3],
+         bounds=[(-1, 4), (None, 5), (0, None)]),                          # shifted / free
+]
+
+
+@pytest.mark.parametrize("case", LP_CASES)
+def test_linprog_adapter_vs_highs(case):
+    from scipy.optimize import linprog as highs
+    from simplex_amd.linprog import linprog as gpu
+    kw = {k: v for k, v in case.items() if k != "c"}
+    a = gpu(case["c"], method="highs-ds", options={"presolve": True, "time_limit": 10}, **kw)
+    b = highs(case["c"], method="highs-ds", **kw)
+    assert a.status == b.status and a.success == b.success
+    if b.status == 0:
+        assert abs(a.fun - b.fun) <= 1e-9 * max(1.0, abs(b.fun))
+
+
+def test_linprog_adapter_random_dense_vs_highs():
+    from scipy.optimize import linprog as highs
+    from simplex_amd.linprog import linprog as gpu
+    rng = np.random.default_rng(5)
+    for k in range(6):
+        m, n = 30 + 7 * k, 20 + 5 * k
+        A = rng.uniform(-1, 2, size=(m, n))
+        b = rng.uniform(1, 10, size=m)
+        c = -rng.uniform(0, 1, size=n)
+        a, h = gpu(c, A_ub=A, b_ub=b), highs(c, A_ub=A, b_ub=b, method="highs-ds")
+        assert a.status == h.status
+        if h.status == 0:
+            assert abs(a.fun - h.fun) <= 1e-9 * max(1.0, abs(h.fun))
+
+
+@pytest.mark.parametrize("engine", ["highs", "gpu"])
+def test_controller_end_to_end_real_solvers(tmp_path, monkeypatch, engine):
+    """reference tests/test_solver_controller.py MAX case, unmocked: the tables
+    come from the GPU pivot engine, the answer from HiGHS or the GPU."""
+    from simplex_amd import storage
+    from simplex_amd.controller import SolverController
+    monkeypatch.setattr(storage, "OUTPUT_DIR", str(tmp_path))
+    wrap = {"problema_definicion": {
+        "funcion_objetivo": {"type": "maximize", "coefficients": {"x1": 15.0, "x2": 18.0}},
+        "restricciones": [
+            {"coefficients": {"x1": 4.0, "x2": 2.0}, "operator": "<=", "rhs": 2000.0},
+            {"coefficients": {"x1": 2.0, "x2": 6.0}, "operator": "<=", "rhs": 2400.0},
+            {"coefficients": {"x1": 20.0, "x2": 28.0}, "operator": "<=", "rhs": 14000.0}]}}
+    rep = SolverController(wrap, answer_engine=engine).run()
+    sol = rep["solucion_encontrada"]
+    assert sol["status"] == "Solucion Factible"
+    assert sol["valor_optimo_z"] == pytest.approx(9833.333333333, rel=1e-9)
+    tabs = rep["tablas_intermedias"]
+    assert [t["pivot"] for t in tabs] == [None, (1, 1), (2, 0), (0, 3)]
+    assert tabs[-1]["table"][-1][-1] == pytest.approx(9833.3333, abs=1e-4)
+    assert "<table" in rep["visualizacion_gilp_html"]
+    assert len(list(tmp_path.iterdir())) == 1
+
+
+def test_config5_degenerate_bland_full_size_first_pivots(eng_cls):
+    """BASELINE config 5 (m = n = 4096 degenerate LP, Bland): basis indices
+    bit-exact after every one of the first pivots vs the oracle."""
+    from simplex_amd import synth
+    m = n = 4096
+    T, basis = synth.full_tableau("degenerate", m, n, 5)
+    ref, rb = T.copy(), basis.copy()
+    seen = []
+    st, hist = O.solve_tableau(ref, rb, rule="bland", max_iters=25,
+                               on_pivot=lambda r, c, _T: seen.append(rb.copy()))
+    with eng_cls(0) as e:
+        e.load(T, basis)
+        del T
+        for k in range(len(hist)):
+            assert e.pivot(rule="bland") == hist[k]
+            assert np.array_equal(e.basis(), seen[k])
+        assert np.array_equal(e.tableau(), ref)
+        # keep going: Bland never cycles; the objective never decreases
+        z0 = e.objective_row()[-1]
+        r = e.solve(rule="bland", max_iters=400)
+        assert r.status in (0, 1) and e.objective_row()[-1] >= z0
