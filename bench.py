@@ -50,6 +50,8 @@ def parse():
                     help="1: the timed region replays one hipGraph with an event pair "
                          "captured around every elimination; 0: direct launches + events")
     ap.add_argument("--ld-pad", type=int, default=-1, help="column padding (doubles)")
+    ap.add_argument("--time-every", type=int, default=8,
+                    help="HIP events around every k-th elimination of the timed region")
     ap.add_argument("--cpu-seconds", type=float, default=15.0,
                     help="budget of the CPU-baseline sample (0 disables)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles",
@@ -143,7 +145,7 @@ def main():
     barrier()
     eng.sync()
     t0 = time.perf_counter()
-    eng.run_pivots(args.steps, time_elim=True, **opts)
+    eng.run_pivots(args.steps, time_elim=args.time_every, **opts)
     eng.sync()
     t1 = time.perf_counter()
     barrier()
@@ -156,13 +158,13 @@ def main():
     if status != 4 or iters != args.warmup + args.steps:
         raise SystemExit(f"pivot loop ended early: status {status}, iters {iters}")
     ms_tot, launches, touched = eng.elim_timing(reset=True)
-    window = ("timed region: HIP event nodes captured around every elimination in the "
-              "replayed hipGraph, on the engine stream" if use_graph else
-              "timed region: HIP events around every elimination launch, engine stream")
+    window = (f"timed region: HIP event-record nodes around every {args.time_every}th "
+              f"elimination inside the replayed hipGraph, on the engine stream" if use_graph else
+              f"timed region: HIP events around every {args.time_every}th elimination launch")
     avg_ms = ms_tot / launches
     m_local = row1 - row0
     N = n + m + 1
-    cols_per_launch = touched / launches
+    cols_per_launch = touched / args.steps  # touched_total counts every pivot
     # algorithmic HBM bytes of one elimination launch: read+write 16 B for every
     # touched element except the entering column, which is only written (8 B)
     alg_bytes = 16.0 * m_local * (cols_per_launch - 1.0) + 8.0 * m_local

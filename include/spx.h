@@ -143,7 +143,8 @@ int spx_pivot(spx_ctx* ctx, const spx_opts* opts, int64_t* r, int64_t* c);
 int spx_pivot_at(spx_ctx* ctx, int64_t r, int64_t c);
 /* Enqueue exactly `npivots` rule-chosen pivots without host synchronisation
  * (benchmark primitive; pivots after termination are no-ops on the device).
- * If `time_elim` is nonzero, HIP events bracket every elimination launch. */
+ * If `time_elim` = k > 0, HIP events bracket every k-th elimination launch
+ * (event-record nodes inside the replayed hipGraph when use_graph is set). */
 int spx_run_pivots(spx_ctx* ctx, const spx_opts* opts, int64_t npivots, int time_elim);
 int spx_sync(spx_ctx* ctx);
 /* Device-side state after spx_sync: status code (SPX_RUNNING while going),

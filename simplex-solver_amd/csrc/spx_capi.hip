@@ -117,6 +117,7 @@ struct spx_ctx {
   hipGraphExec_t texec = nullptr;   // event-timed graph of the last spx_run_pivots
   int64_t tpivots = 0;
   size_t tev0 = 0;                  // first event index the timed graph records
+  int tevery = 0;                   // its sampling period
 
   // elimination timing
   std::vector<std::pair<hipEvent_t, hipEvent_t>> ev;
@@ -838,7 +839,7 @@ int spx_pivot_at(spx_ctx* ctx, int64_t r, int64_t c) {
 
 int spx_run_pivots(spx_ctx* ctx, const spx_opts* opts, int64_t npivots, int time_elim) {
   if (!ctx) return SPX_E_ARG;
-  CHECK_ARG(npivots >= 0, "npivots < 0");
+  CHECK_ARG(npivots >= 0 && time_elim >= 0, "npivots / time_elim < 0");
   spx_opts d;
   spx_default_opts(&d);
   const spx_opts* o = opts ? opts : &d;
@@ -848,7 +849,8 @@ int spx_run_pivots(spx_ctx* ctx, const spx_opts* opts, int64_t npivots, int time
   if (time_elim && graph) {
     // one graph of exactly npivots pivots with an event pair around every
     // elimination; instantiated before it is launched (outside any timing)
-    if (ctx->texec && (ctx->tpivots != npivots || ctx->tev0 != ctx->ev_used)) {
+    if (ctx->texec && (ctx->tpivots != npivots || ctx->tev0 != ctx->ev_used ||
+                       ctx->tevery != time_elim)) {
       (void)hipGraphExecDestroy(ctx->texec);
       ctx->texec = nullptr;
     }
@@ -856,7 +858,8 @@ int spx_run_pivots(spx_ctx* ctx, const spx_opts* opts, int64_t npivots, int time
       const size_t ev0 = ctx->ev_used;
       hipGraph_t g = nullptr;
       HIPC(hipStreamBeginCapture(ctx->stream, hipStreamCaptureModeThreadLocal));
-      for (int64_t i = 0; i < npivots && rc == SPX_OK; ++i) rc = enqueue_pivot(ctx, true);
+      for (int64_t i = 0; i < npivots && rc == SPX_OK; ++i)
+        rc = enqueue_pivot(ctx, i % time_elim == 0);
       hipError_t e = hipStreamEndCapture(ctx->stream, &g);
       if (rc == SPX_OK && e == hipSuccess) e = hipGraphInstantiate(&ctx->texec, g, nullptr, nullptr, 0);
       if (g) (void)hipGraphDestroy(g);
@@ -869,8 +872,9 @@ int spx_run_pivots(spx_ctx* ctx, const spx_opts* opts, int64_t npivots, int time
       }
       ctx->tpivots = npivots;
       ctx->tev0 = ev0;
+      ctx->tevery = time_elim;
     }
-    ctx->ev_used += (size_t)npivots;
+    ctx->ev_used += (size_t)((npivots + time_elim - 1) / time_elim);
     HIPC(hipGraphLaunch(ctx->texec, ctx->stream));
     return SPX_OK;
   }
@@ -883,7 +887,7 @@ int spx_run_pivots(spx_ctx* ctx, const spx_opts* opts, int64_t npivots, int time
       if ((rc = enqueue_pivot(ctx, false))) return rc;
   } else {
     for (int64_t i = 0; i < npivots; ++i)
-      if ((rc = enqueue_pivot(ctx, time_elim != 0))) return rc;
+      if ((rc = enqueue_pivot(ctx, time_elim > 0 && i % time_elim == 0))) return rc;
   }
   return SPX_OK;
 }

@@ -277,6 +277,8 @@ __global__ __launch_bounds__(BLK) void norm_kernel(const double* __restrict__ A,
   const int slot = (int)(it & 1);
   const int64_t c = (MODE == MODE_INIT) ? -1 : st->c_next;
   const int64_t forced_r = st->forced_r;
+  // independent of the leaving row: in flight during the ratio reduction
+  double o = (MODE != MODE_PROW && j < N) ? obj[j] : 0.0;
 
   int64_t r = -1;
   if (MODE == MODE_FUSED || MODE == MODE_PROW) {
@@ -311,7 +313,6 @@ __global__ __launch_bounds__(BLK) void norm_kernel(const double* __restrict__ A,
   KeyR ek = keyr_none();
   const double zc = st->zc_next;
   if (j < N) {
-    double o = obj[j];
     if (MODE != MODE_INIT) {
       double p;
       if (MODE == MODE_FUSED) {

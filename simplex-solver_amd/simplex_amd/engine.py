@@ -227,10 +227,12 @@ class DeviceTableau:
     def pivot_at(self, r: int, c: int) -> None:
         self._check(self._lib.spx_pivot_at(self._ctx, int(r), int(c)), "spx_pivot_at")
 
-    def run_pivots(self, npivots: int, time_elim: bool = False, **kw) -> None:
+    def run_pivots(self, npivots: int, time_elim: int = 0, **kw) -> None:
+        """Enqueue npivots pivots; time_elim = k > 0 brackets every k-th
+        elimination with HIP events (read them with elim_timing)."""
         o = make_opts(**kw)
         self._check(self._lib.spx_run_pivots(self._ctx, ctypes.byref(o), int(npivots),
-                                             1 if time_elim else 0), "spx_run_pivots")
+                                             int(time_elim)), "spx_run_pivots")
 
     def sync(self) -> None:
         self._check(self._lib.spx_sync(self._ctx), "spx_sync")

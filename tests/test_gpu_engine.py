@@ -490,3 +490,25 @@ def test_config5_degenerate_bland_full_size_first_pivots(eng_cls):
         z0 = e.objective_row()[-1]
         r = e.solve(rule="bland", max_iters=400)
         assert r.status in (0, 1) and e.objective_row()[-1] >= z0
+
+
+def test_sharded_rccl_in_timed_graph(eng_cls):
+    """bench.py --gpus N path: RCCL all-gather / all-reduce captured in the
+    event-timed hipGraph (1-rank communicator on the single test GPU)."""
+    from simplex_amd import dist, synth
+    m, n = 600, 900
+    T, basis = synth.full_tableau("dense", m, n, 8)
+    ref, rb = T.copy(), basis.copy()
+    st, hist = O.solve_tableau(ref, rb, max_iters=70)
+    uid = dist.make_unique_id()
+    with dist.ShardedTableau(0, 0, 1, uid) as s:
+        s.load_shard(T[:-1], T[-1], basis, m, 0)
+        s.run_pivots(10, use_graph=True)
+        s.sync()
+        s.elim_timing(reset=True)
+        s.run_pivots(60, time_elim=True, use_graph=True)
+        s.sync()
+        ms, cnt, cols = s.elim_timing(reset=True)
+        assert cnt == 60 and ms > 0
+        assert [tuple(h) for h in s.history().tolist()] == hist
+        assert np.array_equal(s.tableau(), ref)
