@@ -208,7 +208,8 @@ void launch_elim_t(spx_ctx* ctx) {
   hipLaunchKernelGGL((elim_kernel<R, NTL, NTS, ILV>), dim3(ctx->rch * ctx->G), dim3(BLK), 0,
                      ctx->stream, ctx->A, ctx->ld, ctx->m_local, ctx->row0, ctx->N, ctx->F,
                      ctx->P, ctx->list, ctx->rch, ctx->G, ctx->enter_part, ctx->nbn,
-                     ctx->ratio_part, ctx->obj, ctx->basis, ctx->prm, ctx->st);
+                     ctx->ratio_part, ctx->sharded ? ctx->sendkey : nullptr, ctx->obj,
+                     ctx->basis, ctx->prm, ctx->st);
 }
 
 template <int R>
@@ -336,8 +337,11 @@ int enqueue_pivot(spx_ctx* ctx, bool time_elim) {
   if (!ctx->sharded) {
     launch_norm<MODE_FUSED>(ctx, ctx->ratio_part, 0);
   } else {
-    hipLaunchKernelGGL(select_kernel, dim3(1), dim3(BLK), 0, ctx->stream, ctx->ratio_part,
-                       ctx->sendkey, ctx->st);
+    // with one row chunk per rank the previous elimination already wrote the
+    // send key; begin_call runs select once after the priming kernel
+    if (ctx->rch > 1)
+      hipLaunchKernelGGL(select_kernel, dim3(1), dim3(BLK), 0, ctx->stream, ctx->ratio_part,
+                         ctx->sendkey, ctx->st);
     int rc = comm_allgather_keys(ctx);
     if (rc) return rc;
     launch_norm<MODE_PROW>(ctx, ctx->keys_all, ctx->nranks);
@@ -401,6 +405,7 @@ int begin_call(spx_ctx* ctx, const spx_opts* o, int64_t fc = -1, int64_t fr = -1
     ctx->err = "no tableau loaded";
     return SPX_E_STATE;
   }
+  HIPC(hipSetDevice(ctx->device));
   (void)hipGetLastError();  // drop a stale error of an unrelated earlier call
   int rc = pull_state(ctx);
   if (rc) return rc;
@@ -408,6 +413,9 @@ int begin_call(spx_ctx* ctx, const spx_opts* o, int64_t fc = -1, int64_t fr = -1
   if ((rc = set_state_fields(ctx, ST_RUNNING, fc, fr))) return rc;
   launch_norm<MODE_INIT>(ctx, nullptr, 0);
   launch_prime(ctx);
+  if (ctx->sharded && ctx->rch == 1)
+    hipLaunchKernelGGL(select_kernel, dim3(1), dim3(BLK), 0, ctx->stream, ctx->ratio_part,
+                       ctx->sendkey, ctx->st);
   HIPC(hipGetLastError());
   return SPX_OK;
 }

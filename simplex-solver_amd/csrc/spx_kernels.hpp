@@ -387,7 +387,7 @@ __global__ __launch_bounds__(BLK) void select_kernel(const Key* __restrict__ rat
 
 // ---------------------------------------------------------------------------
 // elim_kernel: the rank-1 Gauss-Jordan update (HBM-bound) + the next pivot's
-// ratio test.  grid = rch * G blocks; block b owns row chunk (b % rch) of
+// ratio test (and, on a sharded rank with one row chunk, its all-gather key).  grid = rch * G blocks; block b owns row chunk (b % rch) of
 // RC = BLK*R rows and column group g = b / rch.  Each thread keeps its R values
 // of F in registers and streams R/2 16-B vectors per column, two columns in
 // flight.  Groups 1..G-1 (all groups if G == 1) share the compacted column
@@ -444,8 +444,8 @@ __global__ __launch_bounds__(BLK) void elim_kernel(
     double* __restrict__ A, int64_t ld, int64_t m_local, int64_t row0, int64_t N,
     double* __restrict__ F2, const double* __restrict__ P, const int* __restrict__ list, int rch,
     int G, const Key* __restrict__ enter_part, int nbn, Key* __restrict__ ratio_part,
-    const double* __restrict__ obj, const int64_t* __restrict__ basis,
-    const Params* __restrict__ prm, State* st) {
+    Key* __restrict__ sendkey, const double* __restrict__ obj,
+    const int64_t* __restrict__ basis, const Params* __restrict__ prm, State* st) {
   static_assert(R % 2 == 0, "R must be even");
   using E = Elim<R, NTL, NTS>;
   constexpr int V = R / 2;
@@ -586,7 +586,12 @@ __global__ __launch_bounds__(BLK) void elim_kernel(
       }
     }
     k = block_min(k);
-    if (threadIdx.x == 0) store_key(ratio_part + chunk, k);
+    if (threadIdx.x == 0) {
+      store_key(ratio_part + chunk, k);
+      // sharded rank whose rows are one chunk: this IS the rank's leaving-row
+      // candidate, written straight into the all-gather send buffer
+      if (sendkey != nullptr && rch == 1) store_key(sendkey, k);
+    }
   }
 }
 

@@ -512,3 +512,39 @@ def test_sharded_rccl_in_timed_graph(eng_cls):
         assert cnt == 60 and ms > 0
         assert [tuple(h) for h in s.history().tolist()] == hist
         assert np.array_equal(s.tableau(), ref)
+
+
+def test_config4_eight_virtual_ranks_full_size(eng_cls):
+    """BASELINE config 4: the config-3 tableau (8192 x 16385) row-sharded over
+    8 ranks (1024 rows each), here 8 virtual ranks on one GPU exchanging
+    in-process; first pivots bit-exact vs the oracle on every rank."""
+    from simplex_amd import dist, synth
+    m = n = 8192
+    world, k = 8, 4
+    uid = b"cfg4" + os.urandom(124)
+    outs, errors = {}, []
+
+    def rank_main(rank):
+        try:
+            r0, r1 = dist.row_partition(m, world, rank)
+            Tl, obj, basis = synth.tableau_rows("dense", m, n, 20251205, r0, r1, order="F")
+            with dist.ShardedTableau(0, rank, world, uid, local=True) as s:
+                s.load_shard(Tl, obj, basis, m, r0)
+                s.solve(max_iters=k)
+                outs[rank] = (r0, r1, s.history().tolist(), s.tableau(), s.basis())
+        except Exception as ex:  # pragma: no cover
+            errors.append(ex)
+
+    th = [threading.Thread(target=rank_main, args=(r,)) for r in range(world)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=900)
+    assert not errors, errors
+    T, basis = synth.full_tableau("dense", m, n, 20251205)
+    st, hist = O.solve_tableau(T, basis, max_iters=k)
+    for rank in range(world):
+        r0, r1, h, Tl, b = outs[rank]
+        assert [tuple(x) for x in h] == hist
+        assert np.array_equal(Tl[:-1], T[r0:r1]) and np.array_equal(Tl[-1], T[-1])
+        assert np.array_equal(b, basis)
