@@ -159,7 +159,8 @@ int spx_elim_timing(spx_ctx* ctx, double* total_ms, int64_t* count, int64_t* tou
 
 /* Tuning knob of the elimination kernel: rows per thread R (2, 4, 8; 0 = auto),
  * grid target (0 = auto), non-temporal flags (bit 0 loads, bit 1 stores) and
- * interleaved column assignment (1) instead of contiguous column ranges (0). */
+ * `interleave`: bit 0 = interleaved column assignment (else contiguous column
+ * ranges), bit 1 = disable software pipelining of column pairs. */
 int spx_set_elim_variant(spx_ctx* ctx, int R, int target_wgs, int nt_flags, int interleave);
 /* Layout knob: extra doubles of padding per stored column (even, 0..4096);
   * applies to the next spx_load / spx_load_rows; -1 = automatic. */

@@ -107,6 +107,7 @@ struct spx_ctx {
   int nbn = 1, nbr = 1, rch = 1, G = 1, R = 8;
   int elim_nt = 0;         // bit 0: non-temporal loads, bit 1: non-temporal stores
   int elim_ilv = 1;        // interleaved column assignment
+  int elim_pipe = 1;       // software-pipelined column pairs
   int ld_pad = -1;         // extra doubles per column (-1: auto, 256 for big shards)
   int tune_R = 0;          // 0: automatic
   int tune_wgs = 0;        // 0: automatic (2048)
@@ -203,27 +204,33 @@ void choose_geometry(spx_ctx* ctx) {
   ctx->nbr = (int)std::min<int64_t>(256, std::max<int64_t>(1, (m + 2 * BLK - 1) / (2 * BLK)));
 }
 
-template <int R, bool NTL, bool NTS, bool ILV>
+template <int R, bool NTL, bool NTS, bool ILV, bool PIPE>
 void launch_elim_t(spx_ctx* ctx) {
-  hipLaunchKernelGGL((elim_kernel<R, NTL, NTS, ILV>), dim3(ctx->rch * ctx->G), dim3(BLK), 0,
-                     ctx->stream, ctx->A, ctx->ld, ctx->m_local, ctx->row0, ctx->N, ctx->F,
+  hipLaunchKernelGGL((elim_kernel<R, NTL, NTS, ILV, PIPE>), dim3(ctx->rch * ctx->G), dim3(BLK),
+                     0, ctx->stream, ctx->A, ctx->ld, ctx->m_local, ctx->row0, ctx->N, ctx->F,
                      ctx->P, ctx->list, ctx->rch, ctx->G, ctx->enter_part, ctx->nbn,
                      ctx->ratio_part, ctx->sharded ? ctx->sendkey : nullptr, ctx->obj,
                      ctx->basis, ctx->prm, ctx->st);
 }
 
+template <int R, bool ILV, bool PIPE>
+void launch_elim_nt(spx_ctx* ctx) {
+  switch (ctx->elim_nt & 3) {
+    case 0: launch_elim_t<R, false, false, ILV, PIPE>(ctx); break;
+    case 1: launch_elim_t<R, true, false, ILV, PIPE>(ctx); break;
+    case 2: launch_elim_t<R, false, true, ILV, PIPE>(ctx); break;
+    default: launch_elim_t<R, true, true, ILV, PIPE>(ctx); break;
+  }
+}
+
 template <int R>
 void launch_elim_r(spx_ctx* ctx) {
-  const int v = (ctx->elim_nt & 3) | (ctx->elim_ilv ? 4 : 0);
-  switch (v) {
-    case 0: launch_elim_t<R, false, false, false>(ctx); break;
-    case 1: launch_elim_t<R, true, false, false>(ctx); break;
-    case 2: launch_elim_t<R, false, true, false>(ctx); break;
-    case 3: launch_elim_t<R, true, true, false>(ctx); break;
-    case 4: launch_elim_t<R, false, false, true>(ctx); break;
-    case 5: launch_elim_t<R, true, false, true>(ctx); break;
-    case 6: launch_elim_t<R, false, true, true>(ctx); break;
-    default: launch_elim_t<R, true, true, true>(ctx); break;
+  if (ctx->elim_ilv) {
+    if (ctx->elim_pipe) launch_elim_nt<R, true, true>(ctx);
+    else launch_elim_nt<R, true, false>(ctx);
+  } else {
+    if (ctx->elim_pipe) launch_elim_nt<R, false, true>(ctx);
+    else launch_elim_nt<R, false, false>(ctx);
   }
 }
 
@@ -951,7 +958,8 @@ int spx_set_elim_variant(spx_ctx* ctx, int R, int target_wgs, int nt_flags, int 
   ctx->tune_R = R;
   ctx->tune_wgs = target_wgs;
   ctx->elim_nt = nt_flags & 3;
-  ctx->elim_ilv = interleave ? 1 : 0;
+  ctx->elim_ilv = interleave & 1;
+  ctx->elim_pipe = (interleave & 2) ? 0 : 1;  // bit 1 of `interleave`: disable pipelining
   if (ctx->loaded) {
     choose_geometry(ctx);
     if (ctx->rch > ctx->nbr) {  // ratio_part must hold rch partials

@@ -439,7 +439,52 @@ struct Elim {
   }
 };
 
-template <int R, bool NTL, bool NTS, bool ILV>
+// Walks one column group's share of the compacted list: 64 entries at a time
+// held in lanes (one vector load of list[] + one gather of P[] per window),
+// read with v_readlane so the stream loop issues no dependent scalar loads.
+// Columns c' and RHS are skipped (group 0 owns them).  Wave-uniform.
+struct ListCursor {
+  const int* __restrict__ list;
+  const double* __restrict__ P;
+  int w0, ke, step, q, nwin, jl;
+  double pl;
+  int64_t cn, rhs;
+
+  __device__ void load_window(int lane) {
+    const int kk = w0 + lane * step;
+    jl = -1;
+    pl = 0.0;
+    if (kk < ke) {
+      jl = list[kk];
+      pl = P[jl];
+    }
+    nwin = w0 < ke ? min(64, (ke - w0 + step - 1) / step) : 0;
+    q = 0;
+  }
+
+  __device__ bool next(int& j, double& p, int lane) {
+    for (;;) {
+      for (; q < nwin; ++q) {
+        const int jj = __builtin_amdgcn_readlane(jl, q);
+        if (jj != cn && jj != rhs) {
+          j = jj;
+          p = rdlane(pl, q);
+          ++q;
+          return true;
+        }
+      }
+      if (nwin == 0) return false;
+      w0 += 64 * step;
+      if (w0 >= ke) {
+        nwin = 0;
+        return false;
+      }
+      load_window(lane);
+    }
+  }
+};
+
+template <int R, bool NTL, bool NTS, bool ILV, bool PIPE>
 __global__ __launch_bounds__(BLK) void elim_kernel(
     double* __restrict__ A, int64_t ld, int64_t m_local, int64_t row0, int64_t N,
     double* __restrict__ F2, const double* __restrict__ P, const int* __restrict__ list, int rch,
@@ -486,19 +531,13 @@ __global__ __launch_bounds__(BLK) void elim_kernel(
     }
   }
   const int lane = threadIdx.x & 63;
-  int jl = -1;
-  double pl = 0.0;
-  {
-    const int kk = kb + lane * step;
-    if (kk < ke) {
-      jl = list[kk];
-      pl = P[jl];
-    }
-  }
+  ListCursor cur_l{list, P, kb, ke, step, 0, 0, -1, 0.0, -1, rhs};
+  if (lg >= 0) cur_l.load_window(lane);
 
   // the next pivot's entering column: every block must leave it (and the RHS)
   // to group 0
   const int64_t cn = reduce_keys(enter_part, nbn).row;
+  cur_l.cn = cn;
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     st->iters += 1;
     st->count[cur ^ 1] = 0;
@@ -508,50 +547,49 @@ __global__ __launch_bounds__(BLK) void elim_kernel(
     st->n_ratio_part = rch;
   }
 
-  // ---- the compacted column list, 64 entries at a time held in lanes and
-  // walked with v_readlane (no dependent scalar loads in the stream loop)
+  // ---- this group's columns, two per step; PIPE issues the next pair's loads
+  // before the current pair is computed and stored
   if (lg >= 0) {
     dbl2 scratch[V];
-    for (int w0 = kb; w0 < ke; w0 += 64 * step) {
-      if (w0 != kb) {
-        const int kk = w0 + lane * step;
-        jl = -1;
-        if (kk < ke) {
-          jl = list[kk];
-          pl = P[jl];
-        }
+    int a0 = -1, a1 = -1;
+    double pa0 = 0.0, pa1 = 0.0;
+    bool h0 = cur_l.next(a0, pa0, lane);
+    bool h1 = h0 && cur_l.next(a1, pa1, lane);
+    dbl2 ta0[V], ta1[V];
+    if (h0 && a0 != c) E::load(A + (int64_t)a0 * ld, ta0, ok, base);
+    if (h1 && a1 != c) E::load(A + (int64_t)a1 * ld, ta1, ok, base);
+    while (h0) {
+      int b0 = -1, b1 = -1;
+      double pb0 = 0.0, pb1 = 0.0;
+      const bool g0 = cur_l.next(b0, pb0, lane);
+      const bool g1 = g0 && cur_l.next(b1, pb1, lane);
+      dbl2 tb0[V], tb1[V];
+      if (PIPE) {
+        if (g0 && b0 != c) E::load(A + (int64_t)b0 * ld, tb0, ok, base);
+        if (g1 && b1 != c) E::load(A + (int64_t)b1 * ld, tb1, ok, base);
       }
-      const int nwin = min(64, (ke - w0 + step - 1) / step);
-      int q = 0;
-      for (;;) {
-        int j0 = -1, j1 = -1;
-        double p0 = 0.0, p1 = 0.0;
-        for (; q < nwin && j0 < 0; ++q) {
-          const int j = __builtin_amdgcn_readlane(jl, q);
-          if (j != cn && j != rhs) {
-            j0 = j;
-            p0 = rdlane(pl, q);
-          }
-        }
-        for (; q < nwin && j1 < 0; ++q) {
-          const int j = __builtin_amdgcn_readlane(jl, q);
-          if (j != cn && j != rhs) {
-            j1 = j;
-            p1 = rdlane(pl, q);
-          }
-        }
-        if (j0 < 0) break;
-        double* __restrict__ c0 = A + (int64_t)j0 * ld;
-        double* __restrict__ c1 = A + (int64_t)(j1 < 0 ? j0 : j1) * ld;
-        dbl2 t0[V], t1[V];
-        if (j0 != c) E::load(c0, t0, ok, base);
-        if (j1 >= 0 && j1 != c) E::load(c1, t1, ok, base);
-        if (j0 == c) E::unit(c0, ok, base, rl);
-        else E::update(c0, t0, f, ok, base, rl, p0, scratch);
-        if (j1 >= 0) {
-          if (j1 == c) E::unit(c1, ok, base, rl);
-          else E::update(c1, t1, f, ok, base, rl, p1, scratch);
-        }
+      double* __restrict__ c0 = A + (int64_t)a0 * ld;
+      if (a0 == c) E::unit(c0, ok, base, rl);
+      else E::update(c0, ta0, f, ok, base, rl, pa0, scratch);
+      if (h1) {
+        double* __restrict__ c1 = A + (int64_t)a1 * ld;
+        if (a1 == c) E::unit(c1, ok, base, rl);
+        else E::update(c1, ta1, f, ok, base, rl, pa1, scratch);
+      }
+      if (!PIPE) {
+        if (g0 && b0 != c) E::load(A + (int64_t)b0 * ld, tb0, ok, base);
+        if (g1 && b1 != c) E::load(A + (int64_t)b1 * ld, tb1, ok, base);
+      }
+      a0 = b0;
+      a1 = b1;
+      pa0 = pb0;
+      pa1 = pb1;
+      h0 = g0;
+      h1 = g1;
+#pragma unroll
+      for (int v = 0; v < V; ++v) {
+        ta0[v] = tb0[v];
+        ta1[v] = tb1[v];
       }
     }
   }

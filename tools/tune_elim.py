@@ -15,9 +15,10 @@ from simplex_amd import synth  # noqa: E402
 from simplex_amd.engine import DeviceTableau  # noqa: E402
 
 m = n = int(os.environ.get("TUNE_M", "8192"))
-pads = [int(x) for x in os.environ.get("TUNE_PADS", "256,512,1024").split(",")]
-variants = [(R, wgs, nt, 1) for R in (2, 4) for wgs in (768, 1024, 1280, 1536)
-            for nt in (0, 2, 3)] + [(4, 1280, 0, 0)]
+pads = [int(x) for x in os.environ.get("TUNE_PADS", "256,512").split(",")]
+# (R, grid target, nt flags, interleave bits: 1 = interleaved, +2 = no pipelining)
+variants = [(R, wgs, nt, ilv) for R in (2, 4) for wgs in (1024, 1280, 1536)
+            for nt in (0, 2) for ilv in (1, 3)]
 Tf, obj, basis = synth.tableau_rows("dense", m, n, 20251205, order="F")
 for pad in pads:
     eng = DeviceTableau(0)
