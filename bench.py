@@ -67,27 +67,52 @@ def dist_env():
 
 
 def cpu_baseline(m, n, seed, rule, budget_s, gpu_hist):
-    """Time the numpy oracle on the same tableau (rank 0, N=1)."""
+    """Time the CPU oracle on the same config-3 tableau (rank 0, N=1 only).
+
+    Primary figure: the C/OpenMP restatement (oracle/spx_oracle.c) on all the
+    host threads OpenMP is allowed (OMP_NUM_THREADS).  Also reported: the numpy
+    oracle, 1 thread.  Both must reproduce the GPU's first pivots exactly."""
+    from oracle import c_oracle as C
     from oracle import simplex_oracle as O
     from simplex_amd import synth
-    Tf, obj, basis = synth.tableau_rows("dense", m, n, seed, order="C")
+    Tf, obj, basis0 = synth.tableau_rows("dense", m, n, seed, order="C")
     T = np.vstack([Tf, obj[None, :]])
     del Tf
-    k, t0 = 0, time.perf_counter()
-    hist = []
-    while time.perf_counter() - t0 < budget_s and k < 2000:
-        c = O.select_entering(T[-1], T.shape[1] - 1, rule, 1e-9)
-        r = O.ratio_test(T, c, basis, rule, 1e-12)
-        O.pivot(T, r, c)
-        basis[r] = c
-        hist.append((r, c))
+    out = {}
+    # C / OpenMP
+    Tc, bc = T.copy(), basis0.copy()
+    k, hist, t0 = 0, [], time.perf_counter()
+    while time.perf_counter() - t0 < budget_s and k < 5000:
+        st, h = C.solve(Tc, bc, rule=rule, max_iters=1, hist_cap=1)
+        if st != 1:  # no pivot made (optimal / unbounded)
+            break
+        hist += h
         k += 1
     el = time.perf_counter() - t0
-    match = [tuple(h) for h in gpu_hist[:k]] == hist
-    return {"value": k / el, "unit": "pivots/s", "cores": 1, "kind": "port",
-            "sample": f"numpy oracle (oracle/simplex_oracle.py), first {k} {rule} pivots of the "
-                      f"same {m}x{n} tableau from the slack basis, {el:.1f} s, 1 thread",
-            "pivot_sequence_matches_gpu": bool(match),
+    del Tc
+    kk = min(k, len(gpu_hist))
+    out["c"] = (k, el, [tuple(x) for x in gpu_hist[:kk]] == hist[:kk])
+    # numpy, 1 thread
+    k2, hist2, t0 = 0, [], time.perf_counter()
+    while time.perf_counter() - t0 < budget_s / 3 and k2 < 2000:
+        c = O.select_entering(T[-1], T.shape[1] - 1, rule, 1e-9)
+        r = O.ratio_test(T, c, basis0, rule, 1e-12)
+        O.pivot(T, r, c)
+        basis0[r] = c
+        hist2.append((r, c))
+        k2 += 1
+    el2 = time.perf_counter() - t0
+    kk = min(k2, len(gpu_hist))
+    out["np"] = (k2, el2, [tuple(x) for x in gpu_hist[:kk]] == hist2[:kk])
+    k, el, ok = out["c"]
+    k2, el2, ok2 = out["np"]
+    return {"value": k / el, "unit": "pivots/s", "cores": C.threads(), "kind": "port",
+            "sample": f"C/OpenMP oracle (oracle/spx_oracle.c), first {k} {rule} pivots of the "
+                      f"same {m}x{n} tableau from the slack basis, {el:.1f} s, "
+                      f"{C.threads()} threads",
+            "pivot_sequence_matches_gpu": bool(ok and ok2),
+            "numpy_1thread": {"value": k2 / el2, "pivots": k2, "seconds": el2,
+                              "matches_gpu": bool(ok2)},
             "host": {"cpu_count": os.cpu_count(),
                      "OMP_NUM_THREADS": os.environ.get("OMP_NUM_THREADS"),
                      "model": _cpu_model()}}

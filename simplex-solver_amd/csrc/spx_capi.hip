@@ -105,9 +105,9 @@ struct spx_ctx {
 
   // launch geometry
   int nbn = 1, nbr = 1, rch = 1, G = 1, R = 8;
-  int elim_nt = 0;         // bit 0: non-temporal loads, bit 1: non-temporal stores
+  int elim_nt = 2;         // bit 0: non-temporal loads, bit 1: non-temporal stores
   int elim_ilv = 1;        // interleaved column assignment
-  int elim_pipe = 1;       // software-pipelined column pairs
+  int elim_pipe = 0;       // software-pipelined column pairs (measured neutral)
   int ld_pad = -1;         // extra doubles per column (-1: auto, 256 for big shards)
   int tune_R = 0;          // 0: automatic
   int tune_wgs = 0;        // 0: automatic (2048)
@@ -195,8 +195,10 @@ void choose_geometry(spx_ctx* ctx) {
   if (ctx->tune_R == 2 || ctx->tune_R == 4 || ctx->tune_R == 8) ctx->R = ctx->tune_R;
   const int64_t rc = (int64_t)BLK * ctx->R;
   ctx->rch = (int)std::max<int64_t>(1, (m + rc - 1) / rc);
-  // measured on config 3 (tools/tune_elim.py): ~5 workgroups per CU streaming
-  // interleaved column windows beats a full 8-per-CU grid
+  // measured on config 3 (tools/tune_elim.py, profiles/r01/tune_*.log): five
+  // resident workgroups per CU streaming interleaved column windows with
+  // non-temporal stores (6.6 TB/s) beat a full 8-per-CU grid; a grid that
+  // does not fit in one residency round (1536) leaves a tail
   const int target = ctx->tune_wgs > 0 ? ctx->tune_wgs : 1280;
   ctx->G = std::max(1, target / ctx->rch);
   ctx->G = (int)std::min<int64_t>(ctx->G, std::max<int64_t>(1, ctx->N));

@@ -14,12 +14,14 @@ import numpy as np  # noqa: E402
 from simplex_amd import synth  # noqa: E402
 from simplex_amd.engine import DeviceTableau  # noqa: E402
 
-m = n = int(os.environ.get("TUNE_M", "8192"))
-pads = [int(x) for x in os.environ.get("TUNE_PADS", "256,512").split(",")]
+m = int(os.environ.get("TUNE_M", "8192"))
+n = int(os.environ.get("TUNE_N", str(m)))
+pads = [int(x) for x in os.environ.get("TUNE_PADS", "128,256,384").split(",")]
 # (R, grid target, nt flags, interleave bits: 1 = interleaved, +2 = no pipelining)
-variants = [(R, wgs, nt, ilv) for R in (2, 4) for wgs in (1024, 1280, 1536)
-            for nt in (0, 2) for ilv in (1, 3)]
+variants = [(R, wgs, nt, 3) for R in (2, 4) for wgs in (1024, 1280, 2560)
+            for nt in (2, 3)] + [(4, 1280, 0, 3), (4, 1280, 2, 1), (4, 1280, 2, 2)]
 Tf, obj, basis = synth.tableau_rows("dense", m, n, 20251205, order="F")
+print(json.dumps({"m": m, "n": n, "N": n + m + 1}), flush=True)
 for pad in pads:
     eng = DeviceTableau(0)
     eng.set_ld_pad(pad)
