@@ -157,7 +157,10 @@ def main():
     eng.load_rows(Tf, obj, basis, m, row0)
     del Tf
     if args.nt >= 0 or args.ilv >= 0 or args.R or args.wgs:
-        eng.set_elim_variant(args.R, args.wgs, max(args.nt, 0), args.ilv > 0)
+        v = eng.elim_variant()
+        eng.set_elim_variant(args.R, args.wgs, -1 if args.nt < 0 else args.nt,
+                             (v["interleave"] | (0 if v["pipeline"] else 2)) if args.ilv < 0
+                             else args.ilv)
     opts = dict(rule=args.rule, skip_zero_cols=not args.dense, use_graph=use_graph, chunk=32)
 
     def barrier():
@@ -228,7 +231,7 @@ def main():
                        "m": m, "n": n, "tableau": [m + 1, N], "rule": args.rule,
                        "elimination": "dense sweep" if args.dense else "skip p[j]==0 columns",
                        "timing": "hipGraph replay" if use_graph else "direct launches",
-                       "ld_pad": args.ld_pad,
+                       "elim_variant": eng.elim_variant(),
                        "parallelism": f"row-shard x{world}" if world > 1 else "single GPU"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBPS,

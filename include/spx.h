@@ -158,10 +158,13 @@ int spx_elim_timing(spx_ctx* ctx, double* total_ms, int64_t* count, int64_t* tou
                     int reset);
 
 /* Tuning knob of the elimination kernel: rows per thread R (2, 4, 8; 0 = auto),
- * grid target (0 = auto), non-temporal flags (bit 0 loads, bit 1 stores) and
+ * grid target (0 = auto), non-temporal flags (bit 0 loads, bit 1 stores; -1 = auto) and
  * `interleave`: bit 0 = interleaved column assignment (else contiguous column
  * ranges), bit 1 = disable software pipelining of column pairs. */
 int spx_set_elim_variant(spx_ctx* ctx, int R, int target_wgs, int nt_flags, int interleave);
+/* The elimination variant in use: R, row chunks, column groups, nt flags,
+ * interleave, pipelining, leading dimension. */
+int spx_get_elim_variant(const spx_ctx* ctx, int64_t out[7]);
 /* Layout knob: extra doubles of padding per stored column (even, 0..4096);
   * applies to the next spx_load / spx_load_rows; -1 = automatic. */
 int spx_set_ld_pad(spx_ctx* ctx, int pad);

@@ -105,7 +105,8 @@ struct spx_ctx {
 
   // launch geometry
   int nbn = 1, nbr = 1, rch = 1, G = 1, R = 8;
-  int elim_nt = 2;         // bit 0: non-temporal loads, bit 1: non-temporal stores
+  int elim_nt = 0;         // bit 0: non-temporal loads, bit 1: non-temporal stores
+  int tune_nt = -1;        // -1: automatic (non-temporal stores on tall shards)
   int elim_ilv = 1;        // interleaved column assignment
   int elim_pipe = 0;       // software-pipelined column pairs (measured neutral)
   int ld_pad = -1;         // extra doubles per column (-1: auto, 256 for big shards)
@@ -193,6 +194,9 @@ void choose_geometry(spx_ctx* ctx) {
   const int64_t m = ctx->m_local;
   ctx->R = (m >= 1024) ? 4 : 2;
   if (ctx->tune_R == 2 || ctx->tune_R == 4 || ctx->tune_R == 8) ctx->R = ctx->tune_R;
+  // measured (profiles/r01/tune_m*.log): non-temporal stores win on shards of
+  // >= 4096 rows (6.55 TB/s), plain stores on 1024 / 2048-row shards
+  ctx->elim_nt = ctx->tune_nt >= 0 ? ctx->tune_nt : (m >= 4096 ? 2 : 0);
   const int64_t rc = (int64_t)BLK * ctx->R;
   ctx->rch = (int)std::max<int64_t>(1, (m + rc - 1) / rc);
   // measured on config 3 (tools/tune_elim.py, profiles/r01/tune_*.log): five
@@ -472,7 +476,7 @@ int alloc_common(spx_ctx* ctx, int64_t m_local, int64_t N, int64_t m_global, int
   ctx->m_global = m_global;
   ctx->row0 = row0;
   ctx->N = N;
-  const int pad = ctx->ld_pad >= 0 ? ctx->ld_pad : (m_local >= 2048 ? 256 : 0);
+  const int pad = ctx->ld_pad >= 0 ? ctx->ld_pad : (m_local >= 4096 ? 256 : 0);
   ctx->ld = std::max<int64_t>(64, round_up(m_local, 64)) + pad;
   choose_geometry(ctx);
   ctx->hist_cap = 1 << 20;
@@ -959,17 +963,30 @@ int spx_set_elim_variant(spx_ctx* ctx, int R, int target_wgs, int nt_flags, int 
   if (!ctx) return SPX_E_ARG;
   ctx->tune_R = R;
   ctx->tune_wgs = target_wgs;
-  ctx->elim_nt = nt_flags & 3;
+  ctx->tune_nt = nt_flags < 0 ? -1 : (nt_flags & 3);
   ctx->elim_ilv = interleave & 1;
   ctx->elim_pipe = (interleave & 2) ? 0 : 1;  // bit 1 of `interleave`: disable pipelining
+  choose_geometry(ctx);  // also resolves the automatic nt flags
   if (ctx->loaded) {
-    choose_geometry(ctx);
     if (ctx->rch > ctx->nbr) {  // ratio_part must hold rch partials
       dfree(ctx->ratio_part);
       HIPC(hipMalloc(&ctx->ratio_part, sizeof(Key) * std::max(ctx->nbr, ctx->rch)));
     }
   }
   drop_graphs(ctx);
+  return SPX_OK;
+}
+
+// Variant actually in use: R, rch, G, nt flags, interleave, pipeline, ld.
+int spx_get_elim_variant(const spx_ctx* ctx, int64_t out[7]) {
+  if (!ctx || !out) return SPX_E_ARG;
+  out[0] = ctx->R;
+  out[1] = ctx->rch;
+  out[2] = ctx->G;
+  out[3] = ctx->elim_nt;
+  out[4] = ctx->elim_ilv;
+  out[5] = ctx->elim_pipe;
+  out[6] = ctx->ld;
   return SPX_OK;
 }
 

@@ -251,6 +251,13 @@ class DeviceTableau:
                     "spx_elim_timing")
         return float(ms.value), int(cnt.value), int(cols.value)
 
+    def elim_variant(self) -> dict:
+        out = np.zeros(7, dtype=np.int64)
+        self._check(self._lib.spx_get_elim_variant(self._ctx, _lptr(out)),
+                    "spx_get_elim_variant")
+        keys = ("R", "row_chunks", "col_groups", "nt_flags", "interleave", "pipeline", "ld")
+        return {k: int(v) for k, v in zip(keys, out)}
+
     def set_ld_pad(self, pad: int) -> None:
         """Extra doubles per stored column, applied at the next load."""
         self._check(self._lib.spx_set_ld_pad(self._ctx, int(pad)), "spx_set_ld_pad")
