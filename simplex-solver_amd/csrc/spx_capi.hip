@@ -10,11 +10,11 @@
 // termination / limits.
 //
 // Sharded contexts (spx_create_sharded) split the constraint rows across ranks,
-// one process per GPU.  Per pivot they add one RCCL all-gather of a 32-B
-// leaving-row candidate per rank (the "allreduce-min" of the leaving row:
-// every rank reduces the gathered keys identically) and one RCCL all-reduce
-// of the pivot row (the broadcast from the owner rank, done as a sum with zeros
-// elsewhere so the root never has to be known on the host).
+// one process per GPU.  Per pivot they run ONE RCCL all-gather: every rank
+// contributes [its best leaving-row key | that row normalised]; every rank then
+// takes the lexicographic winner (the leaving-row "allreduce-min", which RCCL
+// has no MINLOC op for) and the winner's row as the pivot row (the owner's
+// broadcast, without a host-known root).
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
@@ -80,7 +80,6 @@ struct spx_ctx {
   ncclComm_t comm = nullptr;
   LoopGroup* loop = nullptr;   // in-process virtual ranks instead of RCCL
   hipEvent_t ev_ready = nullptr, ev_done = nullptr;
-  double* Ptmp = nullptr;      // loop all-reduce output
 
   // dims
   int64_t m_global = 0, m_local = 0, row0 = 0, N = 0, ld = 0;
@@ -96,8 +95,9 @@ struct spx_ctx {
   int64_t* hist = nullptr; // 2 * hist_cap
   Key* enter_part = nullptr;
   Key* ratio_part = nullptr;
-  Key* sendkey = nullptr;
-  Key* keys_all = nullptr;
+  char* sendbuf = nullptr;   // sharded: this rank's all-gather payload
+  char* recvbuf = nullptr;   // sharded: nranks payloads
+  int64_t gstride = 0;       // payload stride (bytes)
   Params* prm = nullptr;
   State* st = nullptr;
   State* h_st = nullptr;   // pinned mirror
@@ -108,7 +108,7 @@ struct spx_ctx {
   int elim_nt = 0;         // bit 0: non-temporal loads, bit 1: non-temporal stores
   int tune_nt = -1;        // -1: automatic (non-temporal stores on tall shards)
   int elim_ilv = 1;        // interleaved column assignment
-  int elim_pipe = 0;       // software-pipelined column pairs (measured neutral)
+  int elim_pipe = 1;       // software-pipelined column pairs (+12% on config 3)
   int ld_pad = -1;         // extra doubles per column (-1: auto, 256 for big shards)
   int tune_R = 0;          // 0: automatic
   int tune_wgs = 0;        // 0: automatic (2048)
@@ -180,9 +180,8 @@ int free_buffers(spx_ctx* ctx) {
   dfree(ctx->hist);
   dfree(ctx->enter_part);
   dfree(ctx->ratio_part);
-  dfree(ctx->sendkey);
-  dfree(ctx->keys_all);
-  dfree(ctx->Ptmp);
+  dfree(ctx->sendbuf);
+  dfree(ctx->recvbuf);
   ctx->loaded = false;
   return SPX_OK;
 }
@@ -215,8 +214,7 @@ void launch_elim_t(spx_ctx* ctx) {
   hipLaunchKernelGGL((elim_kernel<R, NTL, NTS, ILV, PIPE>), dim3(ctx->rch * ctx->G), dim3(BLK),
                      0, ctx->stream, ctx->A, ctx->ld, ctx->m_local, ctx->row0, ctx->N, ctx->F,
                      ctx->P, ctx->list, ctx->rch, ctx->G, ctx->enter_part, ctx->nbn,
-                     ctx->ratio_part, ctx->sharded ? ctx->sendkey : nullptr, ctx->obj,
-                     ctx->basis, ctx->prm, ctx->st);
+                     ctx->ratio_part, ctx->obj, ctx->basis, ctx->prm, ctx->st);
 }
 
 template <int R, bool ILV, bool PIPE>
@@ -249,11 +247,11 @@ void launch_elim(spx_ctx* ctx) {
 }
 
 template <int MODE>
-void launch_norm(spx_ctx* ctx, const Key* keys, int nkeys) {
+void launch_norm(spx_ctx* ctx) {
   hipLaunchKernelGGL((norm_kernel<MODE>), dim3(ctx->nbn), dim3(BLK), 0, ctx->stream, ctx->A,
                      ctx->ld, ctx->m_local, ctx->row0, ctx->N, ctx->obj, ctx->F, ctx->P,
-                     ctx->list, keys, nkeys, ctx->enter_part, ctx->basis, ctx->hist, ctx->prm,
-                     ctx->st);
+                     ctx->list, ctx->ratio_part, ctx->recvbuf, ctx->gstride, ctx->nranks,
+                     ctx->enter_part, ctx->basis, ctx->hist, ctx->prm, ctx->st);
 }
 
 void launch_prime(spx_ctx* ctx) {
@@ -263,18 +261,6 @@ void launch_prime(spx_ctx* ctx) {
 }
 
 constexpr int LOOP_MAX = 16;
-struct PtrArr {
-  double* p[LOOP_MAX];
-};
-
-__global__ __launch_bounds__(BLK) void loop_sum_kernel(PtrArr srcs, int nsrc,
-                                                       double* __restrict__ dst, int64_t n) {
-  const int64_t j = (int64_t)blockIdx.x * BLK + threadIdx.x;
-  if (j >= n) return;
-  double s = 0.0;
-  for (int q = 0; q < nsrc; ++q) s += srcs.p[q][j];
-  dst[j] = s;
-}
 
 int loop_fail(spx_ctx* ctx) {
   ctx->err = "loopback group barrier timed out (a peer rank stopped)";
@@ -290,9 +276,10 @@ int loop_meet(spx_ctx* ctx, hipEvent_t spx_ctx::*ev) {
   return SPX_OK;
 }
 
-int comm_allgather_keys(spx_ctx* ctx) {
+// recvbuf[q] <- sendbuf of rank q, for all q (RCCL, or the in-process group).
+int comm_allgather(spx_ctx* ctx) {
   if (ctx->comm) {
-    NCCLC(ncclAllGather(ctx->sendkey, ctx->keys_all, sizeof(Key), ncclUint8, ctx->comm,
+    NCCLC(ncclAllGather(ctx->sendbuf, ctx->recvbuf, (size_t)ctx->gstride, ncclUint8, ctx->comm,
                         ctx->stream));
     return SPX_OK;
   }
@@ -300,28 +287,9 @@ int comm_allgather_keys(spx_ctx* ctx) {
   int rc = loop_meet(ctx, &spx_ctx::ev_ready);
   if (rc) return rc;
   for (int q = 0; q < G->n; ++q)
-    HIPC(hipMemcpyAsync(ctx->keys_all + q, G->members[q]->sendkey, sizeof(Key),
-                        hipMemcpyDeviceToDevice, ctx->stream));
-  return loop_meet(ctx, &spx_ctx::ev_done);  // peers' sendkey reusable after this
-}
-
-int comm_allreduce_p(spx_ctx* ctx) {
-  if (ctx->comm) {
-    NCCLC(ncclAllReduce(ctx->P, ctx->P, (size_t)ctx->N, ncclDouble, ncclSum, ctx->comm,
-                        ctx->stream));
-    return SPX_OK;
-  }
-  LoopGroup* G = ctx->loop;
-  int rc = loop_meet(ctx, &spx_ctx::ev_ready);
-  if (rc) return rc;
-  PtrArr a;
-  for (int q = 0; q < G->n; ++q) a.p[q] = G->members[q]->P;
-  hipLaunchKernelGGL(loop_sum_kernel, dim3(ctx->nbn), dim3(BLK), 0, ctx->stream, a, G->n,
-                     ctx->Ptmp, ctx->N);
-  if ((rc = loop_meet(ctx, &spx_ctx::ev_done))) return rc;  // peers finished reading my P
-  HIPC(hipMemcpyAsync(ctx->P, ctx->Ptmp, sizeof(double) * ctx->N, hipMemcpyDeviceToDevice,
-                      ctx->stream));
-  return SPX_OK;
+    HIPC(hipMemcpyAsync(ctx->recvbuf + q * ctx->gstride, G->members[q]->sendbuf,
+                        (size_t)ctx->gstride, hipMemcpyDeviceToDevice, ctx->stream));
+  return loop_meet(ctx, &spx_ctx::ev_done);  // peers' sendbuf reusable after this
 }
 
 // Record a timing event on the stream; while the stream is being captured,
@@ -348,18 +316,14 @@ int record_event(spx_ctx* ctx, hipEvent_t ev) {
 // Enqueue one pivot (all launches on ctx->stream; no host synchronisation).
 int enqueue_pivot(spx_ctx* ctx, bool time_elim) {
   if (!ctx->sharded) {
-    launch_norm<MODE_FUSED>(ctx, ctx->ratio_part, 0);
+    launch_norm<MODE_FUSED>(ctx);
   } else {
-    // with one row chunk per rank the previous elimination already wrote the
-    // send key; begin_call runs select once after the priming kernel
-    if (ctx->rch > 1)
-      hipLaunchKernelGGL(select_kernel, dim3(1), dim3(BLK), 0, ctx->stream, ctx->ratio_part,
-                         ctx->sendkey, ctx->st);
-    int rc = comm_allgather_keys(ctx);
+    hipLaunchKernelGGL(prep_kernel, dim3(ctx->nbn), dim3(BLK), 0, ctx->stream, ctx->A, ctx->ld,
+                       ctx->m_local, ctx->row0, ctx->N, ctx->F, ctx->ratio_part, ctx->sendbuf,
+                       ctx->rank, ctx->st);
+    int rc = comm_allgather(ctx);
     if (rc) return rc;
-    launch_norm<MODE_PROW>(ctx, ctx->keys_all, ctx->nranks);
-    if ((rc = comm_allreduce_p(ctx))) return rc;
-    launch_norm<MODE_FINISH>(ctx, nullptr, 0);
+    launch_norm<MODE_FINISH>(ctx);
   }
   if (time_elim) {
     if (ctx->ev_used == ctx->ev.size()) {
@@ -424,11 +388,8 @@ int begin_call(spx_ctx* ctx, const spx_opts* o, int64_t fc = -1, int64_t fr = -1
   if (rc) return rc;
   if ((rc = write_params(ctx, o))) return rc;
   if ((rc = set_state_fields(ctx, ST_RUNNING, fc, fr))) return rc;
-  launch_norm<MODE_INIT>(ctx, nullptr, 0);
+  launch_norm<MODE_INIT>(ctx);
   launch_prime(ctx);
-  if (ctx->sharded && ctx->rch == 1)
-    hipLaunchKernelGGL(select_kernel, dim3(1), dim3(BLK), 0, ctx->stream, ctx->ratio_part,
-                       ctx->sendkey, ctx->st);
   HIPC(hipGetLastError());
   return SPX_OK;
 }
@@ -490,9 +451,12 @@ int alloc_common(spx_ctx* ctx, int64_t m_local, int64_t N, int64_t m_global, int
   HIPC(hipMalloc(&ctx->hist, sizeof(int64_t) * 2 * ctx->hist_cap));
   HIPC(hipMalloc(&ctx->enter_part, sizeof(Key) * ctx->nbn));
   HIPC(hipMalloc(&ctx->ratio_part, sizeof(Key) * std::max(ctx->nbr, ctx->rch)));
-  HIPC(hipMalloc(&ctx->sendkey, sizeof(Key)));
-  HIPC(hipMalloc(&ctx->keys_all, sizeof(Key) * ctx->nranks));
-  if (ctx->loop) HIPC(hipMalloc(&ctx->Ptmp, sizeof(double) * N));
+  if (ctx->sharded) {
+    ctx->gstride = round_up(PAYLOAD_HDR + (int64_t)sizeof(double) * N, 256);
+    HIPC(hipMalloc(&ctx->sendbuf, ctx->gstride));
+    HIPC(hipMalloc(&ctx->recvbuf, ctx->gstride * ctx->nranks));
+    HIPC(hipMemsetAsync(ctx->sendbuf, 0, ctx->gstride, ctx->stream));
+  }
   HIPC(hipMemsetAsync(ctx->A, 0, sizeof(double) * ctx->ld * N, ctx->stream));
   HIPC(hipMemsetAsync(ctx->F, 0, sizeof(double) * 2 * ctx->ld, ctx->stream));
   HIPC(hipMemsetAsync(ctx->P, 0, sizeof(double) * N, ctx->stream));

@@ -18,6 +18,11 @@
 // prime_kernel runs once per host call (after a load / objective change /
 // forced pivot) to produce the first c, F and ratio partials.
 //
+// A row-sharded rank (one process per GPU) runs prep_kernel -> ONE all-gather
+// -> norm_kernel<FINISH> -> elim_kernel per pivot: prep packs this rank's
+// best leaving-row candidate and its normalised row [key | p[0..N)]; after
+// the all-gather every rank takes the lexicographic winner's row as p.
+//
 // Memory layout: the m constraint rows are stored COLUMN-MAJOR
 // (column j is ld contiguous doubles), so the ratio test reads two contiguous
 // columns, the elimination streams whole columns with 16-B lane accesses, and
@@ -244,17 +249,17 @@ __global__ __launch_bounds__(BLK) void prime_kernel(const double* __restrict__ A
 // norm_kernel: one thread per tableau column.
 //   MODE_FUSED  (1 rank): leaving row from ratio partials, p, objective,
 //                         compaction, entering partials, bookkeeping.
-//   MODE_PROW   (sharded, before the p all-reduce): leaving row from the
-//                         all-gathered per-rank keys; the owner writes p,
-//                         the other ranks write zeros.
-//   MODE_FINISH (sharded, after the all-reduce): objective, compaction,
-//                         entering partials, bookkeeping.
+//   MODE_FINISH (sharded, after the all-gather): leaving row = the winner of
+//                         the gathered per-rank keys, p = the winner's row;
+//                         then as FUSED.
 //   MODE_INIT   entering partials only (start of every host call).
 // ---------------------------------------------------------------------------
 constexpr int MODE_FUSED = 0;
-constexpr int MODE_PROW = 1;
 constexpr int MODE_FINISH = 2;
 constexpr int MODE_INIT = 3;
+
+// Layout of one rank's all-gather payload: a Key, then p[0..N).
+constexpr int64_t PAYLOAD_HDR = 32;
 
 template <int MODE>
 __global__ __launch_bounds__(BLK) void norm_kernel(const double* __restrict__ A, int64_t ld,
@@ -262,7 +267,9 @@ __global__ __launch_bounds__(BLK) void norm_kernel(const double* __restrict__ A,
                                                    double* __restrict__ obj,
                                                    const double* __restrict__ F2,
                                                    double* __restrict__ P, int* __restrict__ list,
-                                                   const Key* __restrict__ keys, int nkeys,
+                                                   const Key* __restrict__ keys,
+                                                   const char* __restrict__ gbuf,
+                                                   int64_t gstride, int nranks,
                                                    Key* __restrict__ enter_part,
                                                    int64_t* __restrict__ basis,
                                                    int64_t* __restrict__ hist,
@@ -278,36 +285,51 @@ __global__ __launch_bounds__(BLK) void norm_kernel(const double* __restrict__ A,
   const int64_t c = (MODE == MODE_INIT) ? -1 : st->c_next;
   const int64_t forced_r = st->forced_r;
   // independent of the leaving row: in flight during the ratio reduction
-  double o = (MODE != MODE_PROW && j < N) ? obj[j] : 0.0;
+  double o = (j < N) ? obj[j] : 0.0;
 
   int64_t r = -1;
-  if (MODE == MODE_FUSED || MODE == MODE_PROW) {
+  const double* __restrict__ pw = nullptr;  // FINISH: the winner's p row
+  if (MODE == MODE_FUSED || MODE == MODE_FINISH) {
     if (c < 0 || (forced_r < 0 && it >= prm->iter_limit)) {
       if (blockIdx.x == 0 && threadIdx.x == 0) st->status = (c < 0) ? ST_OPTIMAL : ST_LIMIT;
       return;
     }
-    r = forced_r;
-    if (r < 0) {
-      const KeyR rk = reduce_keys(keys, MODE == MODE_FUSED ? st->n_ratio_part : nkeys);
+    if (MODE == MODE_FUSED) {
+      r = forced_r;
+      if (r < 0) {
+        const KeyR rk = reduce_keys(keys, st->n_ratio_part);
+        if (rk.row < 0) {
+          if (blockIdx.x == 0 && threadIdx.x == 0) st->status = ST_UNBOUNDED;
+          return;
+        }
+        r = rk.row;
+      }
+    } else {
+      // lexicographic winner over the ranks' keys (t is unique, so exactly
+      // one rank's key equals the minimum; its payload holds p)
+      KeyR rk = keyr_none();
+      for (int q = threadIdx.x; q < nranks; q += BLK) {
+        const Key* kq = reinterpret_cast<const Key*>(gbuf + q * gstride);
+        kmin(rk, kq->v, kq->t, kq->row);
+      }
+      rk = block_min(rk);
       if (rk.row < 0) {
         if (blockIdx.x == 0 && threadIdx.x == 0) st->status = ST_UNBOUNDED;
         return;
       }
       r = rk.row;
+      int w = 0;
+      for (int q = 0; q < nranks; ++q) {
+        const Key* kq = reinterpret_cast<const Key*>(gbuf + q * gstride);
+        if (kq->row == r && kq->v == rk.v && kq->t == rk.t) {
+          w = q;
+          break;
+        }
+      }
+      pw = reinterpret_cast<const double*>(gbuf + w * gstride + PAYLOAD_HDR);
     }
   }
   const double* __restrict__ F = F2 + slot * ld;
-
-  if (MODE == MODE_PROW) {
-    const int64_t rl = r - row0;
-    const bool owner = rl >= 0 && rl < m_local;
-    if (j < N) P[j] = owner ? A[j * ld + rl] / F[rl] : 0.0;
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
-      st->r = r;
-      if (owner) st->piv = F[rl];
-    }
-    return;
-  }
 
   bool nz = false;
   KeyR ek = keyr_none();
@@ -315,12 +337,9 @@ __global__ __launch_bounds__(BLK) void norm_kernel(const double* __restrict__ A,
   if (j < N) {
     if (MODE != MODE_INIT) {
       double p;
-      if (MODE == MODE_FUSED) {
-        p = A[j * ld + (r - row0)] / F[r - row0];
-        P[j] = p;
-      } else {
-        p = P[j];
-      }
+      if (MODE == MODE_FUSED) p = A[j * ld + (r - row0)] / F[r - row0];
+      else p = pw[j];
+      P[j] = p;
       nz = (p != 0.0) || !skip;
       if (j == c) {
         o = 0.0;
@@ -360,12 +379,8 @@ __global__ __launch_bounds__(BLK) void norm_kernel(const double* __restrict__ A,
   if (threadIdx.x == 0) store_key(enter_part + blockIdx.x, ek);
 
   if (MODE != MODE_INIT && blockIdx.x == 0 && threadIdx.x == 0) {
-    if (MODE == MODE_FUSED) {
-      st->r = r;
-      st->piv = F[r - row0];
-    } else {
-      r = st->r;
-    }
+    st->r = r;
+    if (r - row0 >= 0 && r - row0 < m_local) st->piv = F[r - row0];
     st->c = c;
     st->zc = zc;
     st->cur = slot;
@@ -377,17 +392,48 @@ __global__ __launch_bounds__(BLK) void norm_kernel(const double* __restrict__ A,
   }
 }
 
-// select_kernel (sharded): this rank's best leaving candidate -> sendkey.
-__global__ __launch_bounds__(BLK) void select_kernel(const Key* __restrict__ ratio_part,
-                                                     Key* __restrict__ sendkey, const State* st) {
+// prep_kernel (sharded rank): this rank's leaving-row candidate for the
+// pending pivot and its normalised row, packed as the all-gather payload
+// [Key (pad = rank) | p[0..N)].  One thread per column.  A forced pivot
+// (spx_pivot_at) is published by the rank that owns the forced row.
+__global__ __launch_bounds__(BLK) void prep_kernel(const double* __restrict__ A, int64_t ld,
+                                                   int64_t m_local, int64_t row0, int64_t N,
+                                                   const double* __restrict__ F2,
+                                                   const Key* __restrict__ ratio_part,
+                                                   char* __restrict__ sendbuf, int rank,
+                                                   const State* st) {
   const bool live = st->status == ST_RUNNING && st->c_next >= 0;
-  const KeyR k = reduce_keys(ratio_part, live ? st->n_ratio_part : 0);
-  if (threadIdx.x == 0) store_key(sendkey, k);
+  const int64_t forced_r = st->forced_r;
+  KeyR k = keyr_none();
+  if (forced_r >= 0) {
+    if (forced_r >= row0 && forced_r < row0 + m_local) k = KeyR{0.0, 0, forced_r};
+  } else {
+    k = reduce_keys(ratio_part, live ? st->n_ratio_part : 0);
+  }
+  const int64_t j = (int64_t)blockIdx.x * BLK + threadIdx.x;
+  const double* __restrict__ F = F2 + (st->iters & 1) * ld;
+  double* __restrict__ p = reinterpret_cast<double*>(sendbuf + PAYLOAD_HDR);
+  if (live && k.row >= 0 && j < N) {
+    const int64_t rl = k.row - row0;
+    p[j] = A[j * ld + rl] / F[rl];
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    Key o;
+    o.v = k.v;
+    o.t = k.t;
+    o.row = live ? k.row : -1;
+    o.pad = rank;
+    if (!live) {
+      o.v = __builtin_inf();
+      o.t = INT64_MAX;
+    }
+    *reinterpret_cast<Key*>(sendbuf) = o;
+  }
 }
 
 // ---------------------------------------------------------------------------
 // elim_kernel: the rank-1 Gauss-Jordan update (HBM-bound) + the next pivot's
-// ratio test (and, on a sharded rank with one row chunk, its all-gather key).  grid = rch * G blocks; block b owns row chunk (b % rch) of
+// ratio test.  grid = rch * G blocks; block b owns row chunk (b % rch) of
 // RC = BLK*R rows and column group g = b / rch.  Each thread keeps its R values
 // of F in registers and streams R/2 16-B vectors per column, two columns in
 // flight.  Groups 1..G-1 (all groups if G == 1) share the compacted column
@@ -489,8 +535,8 @@ __global__ __launch_bounds__(BLK) void elim_kernel(
     double* __restrict__ A, int64_t ld, int64_t m_local, int64_t row0, int64_t N,
     double* __restrict__ F2, const double* __restrict__ P, const int* __restrict__ list, int rch,
     int G, const Key* __restrict__ enter_part, int nbn, Key* __restrict__ ratio_part,
-    Key* __restrict__ sendkey, const double* __restrict__ obj,
-    const int64_t* __restrict__ basis, const Params* __restrict__ prm, State* st) {
+    const double* __restrict__ obj, const int64_t* __restrict__ basis,
+    const Params* __restrict__ prm, State* st) {
   static_assert(R % 2 == 0, "R must be even");
   using E = Elim<R, NTL, NTS>;
   constexpr int V = R / 2;
@@ -624,12 +670,7 @@ __global__ __launch_bounds__(BLK) void elim_kernel(
       }
     }
     k = block_min(k);
-    if (threadIdx.x == 0) {
-      store_key(ratio_part + chunk, k);
-      // sharded rank whose rows are one chunk: this IS the rank's leaving-row
-      // candidate, written straight into the all-gather send buffer
-      if (sendkey != nullptr && rch == 1) store_key(sendkey, k);
-    }
+    if (threadIdx.x == 0) store_key(ratio_part + chunk, k);
   }
 }
 

@@ -262,10 +262,11 @@ class DeviceTableau:
         """Extra doubles per stored column, applied at the next load."""
         self._check(self._lib.spx_set_ld_pad(self._ctx, int(pad)), "spx_set_ld_pad")
 
-    def set_elim_variant(self, R: int = 0, target_wgs: int = 0, nt_flags: int = 0,
-                         interleave: bool = False) -> None:
+    def set_elim_variant(self, R: int = 0, target_wgs: int = 0, nt_flags: int = -1,
+                         interleave: int = 1) -> None:
         """Elimination-kernel tuning: rows per thread, grid target, non-temporal
-        flags (1 loads, 2 stores), interleaved column assignment."""
+        flags (1 loads, 2 stores, -1 auto), interleave bits (1 interleaved
+        columns, +2 disables software pipelining)."""
         self._check(self._lib.spx_set_elim_variant(self._ctx, int(R), int(target_wgs),
-                                                   int(nt_flags), 1 if interleave else 0),
+                                                   int(nt_flags), int(interleave)),
                     "spx_set_elim_variant")
