@@ -6,10 +6,10 @@ with torch.distributed collectives, so the protocol can be checked on CPU
 (gloo, world size >= 2) against the single-process oracle:
 
   1. entering column: chosen locally from the replicated objective row;
-  2. leaving row: each rank's best (ratio, tie, global row) key, all-gathered,
-     lexicographic min taken identically by every rank (RCCL has no MINLOC);
-  3. pivot row: owner computes p = T[r,:]/T[r,c], others contribute zeros,
-     all-reduce(sum) delivers p everywhere (exactly one nonzero term);
+  2. each rank packs [its best (ratio, tie, global row) key | that row
+     normalised by its pivot-column entry] (prep_kernel);
+  3. ONE all-gather of the packs; every rank takes the lexicographic winner
+     (RCCL has no MINLOC) and the winner's row as p (norm_kernel<FINISH>);
   4. elimination of the local rows + the replicated objective row.
 The reference has no distributed code; the single-process
 semantics it must reproduce are those of simplex_oracle.py.
@@ -37,11 +37,11 @@ def local_key(T_loc, row0, c, basis, rule, eps_piv):
     return best
 
 
-def sharded_solve(T_loc, obj, basis, row0, allgather, allreduce_sum, rule="dantzig",
-                  eps_opt=1e-9, eps_piv=1e-12, max_iters=0):
+def sharded_solve(T_loc, obj, basis, row0, allgather, rule="dantzig", eps_opt=1e-9,
+                  eps_piv=1e-12, max_iters=0):
     """T_loc: this rank's constraint rows (m_local x N); obj: replicated
-    objective row; allgather(np.array([ratio, tie, row])) -> list per rank;
-    allreduce_sum(np.ndarray) -> summed array.  Mutates T_loc, obj, basis."""
+    objective row; allgather(np.ndarray) -> list of every rank's array.
+    Mutates T_loc, obj, basis.  Returns (status, [(r, c), ...])."""
     N = obj.shape[0]
     m_local = T_loc.shape[0]
     hist = []
@@ -52,15 +52,19 @@ def sharded_solve(T_loc, obj, basis, row0, allgather, allreduce_sum, rule="dantz
         if c is None:
             return OPTIMAL, hist
         k = local_key(T_loc, row0, c, basis, rule, eps_piv)
-        keys = allgather(np.array([k[0], float(k[1]), float(k[2])]))
-        best = min(((float(a[0]), int(a[1]), int(a[2])) for a in keys), key=lambda t: t[:2])
-        if best[2] < 0:
+        pack = np.zeros(3 + N)
+        pack[:3] = [k[0], float(k[1]), float(k[2])]
+        if k[2] >= 0:
+            rl = k[2] - row0
+            pack[3:] = T_loc[rl, :] / T_loc[rl, c]
+        packs = allgather(pack)
+        w = min(range(len(packs)), key=lambda q: (float(packs[q][0]), int(packs[q][1])))
+        if int(packs[w][2]) < 0:
             return UNBOUNDED, hist
-        r = best[2]
+        r = int(packs[w][2])
+        p = packs[w][3:]
         rl = r - row0
         owner = 0 <= rl < m_local
-        p = T_loc[rl, :] / T_loc[rl, c] if owner else np.zeros(N)
-        p = allreduce_sum(p)
         f = T_loc[:, c].copy()
         zc = obj[c]
         cols = np.flatnonzero(p != 0.0)

@@ -3,15 +3,13 @@
 Partitioning: constraint rows 0..m-1 are split into contiguous
 blocks, one per rank; the objective row and the basis are replicated.  Every
 rank chooses the entering column locally (identical objective rows give
-identical choices, no collective).  Per pivot libspx issues two RCCL calls on
-the context's stream, both captured in the pivot-chunk hipGraph:
-  1. all-gather of each rank's best (ratio, tie, row) key (32 B per rank) —
-     every rank reduces the gathered keys identically (the leaving-row
-     "allreduce-min", which RCCL has no MINLOC op for);
-  2. all-reduce(sum) of the normalised pivot row, non-owners contributing
-     zeros — the owner's broadcast without a host-known root.
-Results are bit-identical to one GPU (the update is elementwise; the sum has
-exactly one nonzero term per element).
+identical choices, no collective).  Per pivot libspx issues ONE RCCL
+all-gather on the context's stream (captured in the pivot-chunk hipGraph):
+each rank contributes [its best (ratio, tie, row) key | that row normalised];
+every rank takes the lexicographic winner (the leaving-row "allreduce-min",
+which RCCL has no MINLOC op for) and the winner's row as the pivot row (the
+owner's broadcast without a host-known root).  Results are bit-identical to
+one GPU.
 
 torch.distributed is used only to ship the 128-byte RCCL unique id from rank 0
 to the others (any backend: gloo on CPU, nccl on GPU).

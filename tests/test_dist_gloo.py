@@ -2,9 +2,10 @@
 
 Covers the host side of simplex_amd.dist (row partition, RCCL unique-id
 exchange through torch.distributed) and the per-pivot exchange protocol that
-libspx runs over RCCL (oracle/sharded_oracle.py restates it with gloo
-collectives): the sharded run must reproduce the single-process oracle's
-pivot sequence and every tableau bit.
+libspx runs over RCCL, one all-gather of [leaving key | normalised row] per
+pivot (oracle/sharded_oracle.py restates it with gloo collectives): the
+sharded run must reproduce the single-process oracle's pivot sequence and
+every tableau bit.
 """
 import os
 import socket
@@ -45,13 +46,7 @@ def _worker(rank, world, port, kind, m, n, seed, rule, q):
             dist.all_gather(out, t)
             return [o.numpy() for o in out]
 
-        def allreduce_sum(a):
-            t = torch.from_numpy(np.ascontiguousarray(a))
-            dist.all_reduce(t, op=dist.ReduceOp.SUM)
-            return t.numpy()
-
-        st, hist = sharded_solve(T, obj, basis, r0, allgather, allreduce_sum, rule=rule,
-                                 max_iters=5000)
+        st, hist = sharded_solve(T, obj, basis, r0, allgather, rule=rule, max_iters=5000)
         q.put((rank, r0, r1, st, hist, T, obj, basis))
     finally:
         dist.destroy_process_group()
