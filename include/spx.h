@@ -160,7 +160,8 @@ int spx_elim_timing(spx_ctx* ctx, double* total_ms, int64_t* count, int64_t* tou
 /* Tuning knob of the elimination kernel: rows per thread R (2, 4, 8; 0 = auto),
  * grid target (0 = auto), non-temporal flags (bit 0 loads, bit 1 stores; -1 = auto) and
  * `interleave`: bit 0 = interleaved column assignment (else contiguous column
- * ranges), bit 1 = disable software pipelining of column pairs. */
+ * ranges), bit 1 = disable software pipelining of column pairs, bit 2 = XCD-aware
+ * block swizzle. */
 int spx_set_elim_variant(spx_ctx* ctx, int R, int target_wgs, int nt_flags, int interleave);
 /* The elimination variant in use: R, row chunks, column groups, nt flags,
  * interleave, pipelining, leading dimension. */

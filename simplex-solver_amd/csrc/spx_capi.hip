@@ -109,6 +109,7 @@ struct spx_ctx {
   int tune_nt = -1;        // -1: automatic (non-temporal stores on tall shards)
   int elim_ilv = 1;        // interleaved column assignment
   int elim_pipe = 1;       // software-pipelined column pairs (+12% on config 3)
+  int elim_xcd = 0;        // XCD-aware block swizzle
   int ld_pad = -1;         // extra doubles per column (-1: auto, 256 for big shards)
   int tune_R = 0;          // 0: automatic
   int tune_wgs = 0;        // 0: automatic (2048)
@@ -214,7 +215,7 @@ void launch_elim_t(spx_ctx* ctx) {
   hipLaunchKernelGGL((elim_kernel<R, NTL, NTS, ILV, PIPE>), dim3(ctx->rch * ctx->G), dim3(BLK),
                      0, ctx->stream, ctx->A, ctx->ld, ctx->m_local, ctx->row0, ctx->N, ctx->F,
                      ctx->P, ctx->list, ctx->rch, ctx->G, ctx->enter_part, ctx->nbn,
-                     ctx->ratio_part, ctx->obj, ctx->basis, ctx->prm, ctx->st);
+                     ctx->ratio_part, ctx->obj, ctx->basis, ctx->prm, ctx->st, ctx->elim_xcd);
 }
 
 template <int R, bool ILV, bool PIPE>
@@ -930,6 +931,7 @@ int spx_set_elim_variant(spx_ctx* ctx, int R, int target_wgs, int nt_flags, int 
   ctx->tune_nt = nt_flags < 0 ? -1 : (nt_flags & 3);
   ctx->elim_ilv = interleave & 1;
   ctx->elim_pipe = (interleave & 2) ? 0 : 1;  // bit 1 of `interleave`: disable pipelining
+  ctx->elim_xcd = (interleave & 4) ? 1 : 0;   // bit 2: XCD-aware block swizzle
   choose_geometry(ctx);  // also resolves the automatic nt flags
   if (ctx->loaded) {
     if (ctx->rch > ctx->nbr) {  // ratio_part must hold rch partials
@@ -949,7 +951,7 @@ int spx_get_elim_variant(const spx_ctx* ctx, int64_t out[7]) {
   out[2] = ctx->G;
   out[3] = ctx->elim_nt;
   out[4] = ctx->elim_ilv;
-  out[5] = ctx->elim_pipe;
+  out[5] = ctx->elim_pipe | (ctx->elim_xcd << 1);
   out[6] = ctx->ld;
   return SPX_OK;
 }

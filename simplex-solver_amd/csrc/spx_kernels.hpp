@@ -536,7 +536,7 @@ __global__ __launch_bounds__(BLK) void elim_kernel(
     double* __restrict__ F2, const double* __restrict__ P, const int* __restrict__ list, int rch,
     int G, const Key* __restrict__ enter_part, int nbn, Key* __restrict__ ratio_part,
     const double* __restrict__ obj, const int64_t* __restrict__ basis,
-    const Params* __restrict__ prm, State* st) {
+    const Params* __restrict__ prm, State* st, int xcd_swz) {
   static_assert(R % 2 == 0, "R must be even");
   using E = Elim<R, NTL, NTS>;
   constexpr int V = R / 2;
@@ -547,8 +547,13 @@ __global__ __launch_bounds__(BLK) void elim_kernel(
   const int64_t rl = st->r - row0;
   const int64_t rhs = N - 1;
   const bool skip = prm->skip_zero != 0;
-  const int chunk = blockIdx.x % rch;
-  const int g = blockIdx.x / rch;
+  // xcd_swz: blocks are dealt round-robin over the 8 XCDs, so remap physical
+  // block b to logical (b % 8) * (grid / 8) + b / 8: each XCD then streams
+  // whole columns (all row chunks) instead of one chunk of every column
+  int bid = blockIdx.x;
+  if (xcd_swz && (gridDim.x & 7) == 0) bid = (blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3);
+  const int chunk = bid % rch;
+  const int g = bid / rch;
   const double* __restrict__ F = F2 + cur * ld;
 
   // Issue the loads that do not depend on c' first (pivot-column values of

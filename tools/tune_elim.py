@@ -18,8 +18,8 @@ m = int(os.environ.get("TUNE_M", "8192"))
 n = int(os.environ.get("TUNE_N", str(m)))
 pads = [int(x) for x in os.environ.get("TUNE_PADS", "256").split(",")]
 # (R, grid target, nt flags, interleave bits: 1 = interleaved, +2 = no pipelining)
-variants = [(4, 1280, nt, ilv) for nt in (0, 2) for ilv in (0, 1, 2, 3)] + \
-    [(R, wgs, 2, 1) for R in (2, 8) for wgs in (1280, 2560)] + [(4, 1024, 2, 1), (4, 1536, 2, 1)]
+variants = [(4, 1280, 2, 1), (4, 1280, 2, 5), (4, 1280, 0, 1), (4, 1280, 0, 5),
+            (4, 2560, 2, 5), (8, 1280, 2, 5), (4, 1024, 2, 5)]
 Tf, obj, basis = synth.tableau_rows("dense", m, n, 20251205, order="F")
 print(json.dumps({"m": m, "n": n, "N": n + m + 1}), flush=True)
 for pad in pads:
