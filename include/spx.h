@@ -126,6 +126,12 @@ int spx_get_tableau(spx_ctx* ctx, double* out, int64_t ld, int layout);
 int spx_get_objective(spx_ctx* ctx, double* out);      /* N values */
 int spx_get_basis(spx_ctx* ctx, int64_t* out);         /* m_global values */
 int spx_get_column(spx_ctx* ctx, int64_t j, double* out); /* local rows of column j */
+int spx_get_row(spx_ctx* ctx, int64_t i, double* out);    /* N values of local row i */
+/* Phase-2 objective row computed on the device from the current tableau:
+ * obj = -cost + sum_i cost[basis[i]] * T[i,:] (cost has N-1 entries, RHS
+ * cost 0), accumulated in row order (bit-identical to the host formula).
+ * Single-GPU contexts only. */
+int spx_set_phase2_objective(spx_ctx* ctx, const double* cost);
 /* Pivot history of the context since load: up to `cap` (row, col) pairs,
  * returns the number of pivots recorded in *n. */
 int spx_get_history(spx_ctx* ctx, int64_t* rc_pairs, int64_t cap, int64_t* n);

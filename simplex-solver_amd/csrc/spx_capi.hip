@@ -943,6 +943,39 @@ int spx_set_elim_variant(spx_ctx* ctx, int R, int target_wgs, int nt_flags, int 
   return SPX_OK;
 }
 
+int spx_get_row(spx_ctx* ctx, int64_t i, double* out) {
+  if (!ctx) return SPX_E_ARG;
+  CHECK_ARG(ctx->loaded && out && i >= 0 && i < ctx->m_local, "bad row");
+  HIPC(hipSetDevice(ctx->device));
+  double* d = nullptr;
+  HIPC(hipMallocAsync(reinterpret_cast<void**>(&d), sizeof(double) * ctx->N, ctx->stream));
+  hipLaunchKernelGGL(get_row_kernel, dim3(ctx->nbn), dim3(BLK), 0, ctx->stream, ctx->A, ctx->ld,
+                     ctx->N, i, d);
+  HIPC(hipGetLastError());
+  HIPC(hipMemcpyAsync(out, d, sizeof(double) * ctx->N, hipMemcpyDeviceToHost, ctx->stream));
+  HIPC(hipFreeAsync(d, ctx->stream));
+  HIPC(hipStreamSynchronize(ctx->stream));
+  return SPX_OK;
+}
+
+int spx_set_phase2_objective(spx_ctx* ctx, const double* cost) {
+  if (!ctx) return SPX_E_ARG;
+  CHECK_ARG(ctx->loaded && cost, "no tableau / null cost");
+  CHECK_ARG(!ctx->sharded, "phase-2 objective of a sharded tableau is not supported");
+  HIPC(hipSetDevice(ctx->device));
+  double* d = nullptr;
+  const size_t nc = (size_t)std::max<int64_t>(1, ctx->N - 1);
+  HIPC(hipMallocAsync(reinterpret_cast<void**>(&d), sizeof(double) * nc, ctx->stream));
+  HIPC(hipMemcpyAsync(d, cost, sizeof(double) * (ctx->N - 1), hipMemcpyHostToDevice,
+                      ctx->stream));
+  hipLaunchKernelGGL(phase2_obj_kernel, dim3(ctx->nbn), dim3(BLK), 0, ctx->stream, ctx->A,
+                     ctx->ld, ctx->m_local, ctx->N, d, ctx->basis, ctx->obj);
+  HIPC(hipGetLastError());
+  HIPC(hipFreeAsync(d, ctx->stream));
+  HIPC(hipStreamSynchronize(ctx->stream));
+  return SPX_OK;
+}
+
 // Variant actually in use: R, rch, G, nt flags, interleave, pipeline, ld.
 int spx_get_elim_variant(const spx_ctx* ctx, int64_t out[7]) {
   if (!ctx || !out) return SPX_E_ARG;

@@ -679,4 +679,36 @@ __global__ __launch_bounds__(BLK) void elim_kernel(
   }
 }
 
+// ---------------------------------------------------------------------------
+// Utility kernels (outside the pivot loop).
+// ---------------------------------------------------------------------------
+// out[j] = T[i, j] for one local constraint row (strided gather).
+__global__ __launch_bounds__(BLK) void get_row_kernel(const double* __restrict__ A, int64_t ld,
+                                                      int64_t N, int64_t i,
+                                                      double* __restrict__ out) {
+  const int64_t j = (int64_t)blockIdx.x * BLK + threadIdx.x;
+  if (j < N) out[j] = A[j * ld + i];
+}
+
+// Phase-2 objective row: obj[j] = -cost[j] + sum_i cost[basis[i]] * T[i, j]
+// (obj[N-1] = 0 + sum_i cost[basis[i]] * b_i), accumulated in row order i =
+// 0..m-1 with a rounded product and a rounded sum per term, skipping rows whose
+// basic cost is zero: bit-identical to simplex_amd.lp.phase2_objective and the
+// oracle.  One thread per column walks its column contiguously.
+__global__ __launch_bounds__(BLK) void phase2_obj_kernel(const double* __restrict__ A,
+                                                         int64_t ld, int64_t m, int64_t N,
+                                                         const double* __restrict__ cost,
+                                                         const int64_t* __restrict__ basis,
+                                                         double* __restrict__ obj) {
+  const int64_t j = (int64_t)blockIdx.x * BLK + threadIdx.x;
+  if (j >= N) return;
+  double s = (j < N - 1) ? -cost[j] : 0.0;
+  const double* __restrict__ col = A + j * ld;
+  for (int64_t i = 0; i < m; ++i) {
+    const double cb = cost[basis[i]];
+    if (cb != 0.0) s = __dadd_rn(s, __dmul_rn(cb, col[i]));
+  }
+  obj[j] = s;
+}
+
 }  // namespace spx

@@ -85,6 +85,8 @@ SIGNATURES = {
     "spx_get_objective": (ctypes.c_int, [_P, _DP]),
     "spx_get_basis": (ctypes.c_int, [_P, _LP]),
     "spx_get_column": (ctypes.c_int, [_P, _I64, _DP]),
+    "spx_get_row": (ctypes.c_int, [_P, _I64, _DP]),
+    "spx_set_phase2_objective": (ctypes.c_int, [_P, _DP]),
     "spx_get_history": (ctypes.c_int, [_P, _LP, _I64, _LP]),
     "spx_dims": (ctypes.c_int, [_P, _LP, _LP, _LP, _LP]),
     "spx_solve": (ctypes.c_int, [_P, ctypes.POINTER(SpxOpts), ctypes.POINTER(SpxResult)]),

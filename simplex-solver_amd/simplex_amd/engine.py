@@ -192,6 +192,19 @@ class DeviceTableau:
         self._check(self._lib.spx_get_column(self._ctx, int(j), _dptr(out)), "spx_get_column")
         return out
 
+    def row(self, i: int) -> np.ndarray:
+        out = np.empty(self.N, dtype=np.float64)
+        self._check(self._lib.spx_get_row(self._ctx, int(i), _dptr(out)), "spx_get_row")
+        return out
+
+    def set_phase2_objective(self, cost) -> None:
+        """obj = -cost + sum_i cost[basis[i]] * T[i,:] on the device (row order)."""
+        cost = np.ascontiguousarray(np.asarray(cost, dtype=np.float64).reshape(-1))
+        if cost.shape[0] != self.N - 1:
+            raise ValueError("cost must have N-1 entries")
+        self._check(self._lib.spx_set_phase2_objective(self._ctx, _dptr(cost)),
+                    "spx_set_phase2_objective")
+
     def history(self) -> np.ndarray:
         """(k, 2) int64 array of (row, col) pivots since load."""
         n = ctypes.c_int64()

@@ -225,26 +225,23 @@ def solve_standard_form(sf: StandardForm, *, device: int = 0, rule: str = "dantz
             if res.status == L.SPX_ITER_LIMIT:
                 return LPResult(L.SPX_ITER_LIMIT, None, None, iters, eng.basis(), pivots,
                                 rec.steps)
-            T = eng.tableau()
             bmax = float(np.max(np.abs(sf.T[:sf.m, -1]))) if sf.m else 0.0
-            if T[-1, -1] < -1e-9 * (1.0 + bmax):
+            if eng.objective_row()[-1] < -1e-9 * (1.0 + bmax):
                 return LPResult(L.SPX_INFEASIBLE, None, None, iters, eng.basis(), pivots,
                                 rec.steps)
+            # drive basic artificials (at zero level) out, one device row at a time
             basis = eng.basis()
             for i in range(sf.m):
                 if basis[i] >= sf.n_enter:
-                    row = T[i, :sf.n_enter]
-                    cand = np.flatnonzero(np.abs(row) > DRIVE_OUT_TOL)
+                    cand = np.flatnonzero(np.abs(eng.row(i)[:sf.n_enter]) > DRIVE_OUT_TOL)
                     if cand.size:
                         j = int(cand[0])
                         eng.pivot_at(i, j)
                         iters += 1
                         pivots.append((1, i, j))
                         rec.record(i, j, 1)
-                        T = eng.tableau()
                         basis = eng.basis()
-            obj2 = phase2_objective(T, basis, sf.cost)
-            eng.set_objective(obj2)
+            eng.set_phase2_objective(sf.cost)  # == phase2_objective(T, basis, cost)
             rec.record(None, None, 2)
         res = _run_phase(eng, rec, 2, rule, sf.n_enter,
                          (max_iters - iters) if max_iters > 0 else 0, time_limit, pivots)

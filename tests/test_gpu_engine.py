@@ -548,3 +548,23 @@ def test_config4_eight_virtual_ranks_full_size(eng_cls):
         assert [tuple(x) for x in h] == hist
         assert np.array_equal(Tl[:-1], T[r0:r1]) and np.array_equal(Tl[-1], T[-1])
         assert np.array_equal(b, basis)
+
+
+def test_device_phase2_objective_and_row_gather_match_host(eng_cls):
+    from simplex_amd import lp
+    rng = np.random.default_rng(12)
+    m, N = 37, 90
+    T = rng.normal(size=(m + 1, N))
+    T[rng.random(T.shape) < 0.2] = 0.0
+    basis = rng.permutation(N - 1)[:m].astype(np.int64)
+    cost = rng.normal(size=N - 1)
+    cost[rng.random(N - 1) < 0.3] = 0.0
+    with eng_cls(0) as e:
+        e.load(T, basis)
+        for i in (0, 5, m - 1):
+            assert e.row(i).tobytes() == T[i].tobytes()
+        e.set_phase2_objective(cost)
+        got = e.objective_row()
+    ref = lp.phase2_objective(T, basis, cost)
+    assert got.tobytes() == ref.tobytes()
+    assert np.array_equal(ref, O.phase2_row(T, basis, cost))
