@@ -1,0 +1,81 @@
+"""Timings of the BASELINE.json configs other than the headline (bench.py is
+config 3 / 4).  One JSON line per config:
+
+  config 2: 1024 x 2048 dense random-feasible LP, full Dantzig solve on one GPU
+            (wall time of spx_solve, hipGraph chunks), vs the C/OpenMP oracle's
+            full solve and HiGHS (linprog 'highs-ds', the reference's answer
+            path, solver_controller.py:78-85) on the host.
+  config 5: degenerate 4096 x 4096 LP, Bland's rule: pivots/s over K pivots on
+            one GPU vs the C/OpenMP oracle over its first pivots (same
+            sequence checked).
+Both GPU results are checked against the oracle (objective / pivot sequence).
+"""
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "simplex-solver_amd"))
+sys.path.insert(0, ROOT)
+import numpy as np  # noqa: E402
+
+from oracle import c_oracle as C  # noqa: E402
+from simplex_amd import synth  # noqa: E402
+from simplex_amd.engine import DeviceTableau  # noqa: E402
+
+
+def config2():
+    m, n, seed = 1024, 2048, 20251207
+    T, basis = synth.full_tableau("dense", m, n, seed)
+    with DeviceTableau(0) as e:
+        e.load(T, basis)
+        e.solve(max_iters=5)  # warm: graph build, first launches
+        e.load(T, basis)
+        t0 = time.perf_counter()
+        res = e.solve()
+        gpu_s = time.perf_counter() - t0
+        hist = e.history().tolist()
+    Tc, bc = T.copy(), basis.copy()
+    t0 = time.perf_counter()
+    st, hc = C.solve(Tc, bc)
+    cpu_s = time.perf_counter() - t0
+    from scipy.optimize import linprog
+    A, b, c = synth.lp_data("dense", m, n, seed)
+    t0 = time.perf_counter()
+    h = linprog(-c, A_ub=A, b_ub=b, bounds=[(0, None)] * n, method="highs-ds")
+    highs_s = time.perf_counter() - t0
+    return {"config": "2: 1024x2048 dense LP, full Dantzig solve", "gpu_s": gpu_s,
+            "pivots": res.iters, "gpu_pivots_per_s": res.iters / gpu_s,
+            "objective": res.objective, "highs_objective": -h.fun, "highs_s": highs_s,
+            "highs_nit": int(h.nit), "cpu_oracle_s": cpu_s, "cpu_threads": C.threads(),
+            "sequence_matches_oracle": [tuple(x) for x in hist] == hc,
+            "objective_rel_err_vs_highs": abs(res.objective + h.fun) / abs(h.fun)}
+
+
+def config5(k=2000, k_cpu=60):
+    m = n = 4096
+    T, basis = synth.full_tableau("degenerate", m, n, 5)
+    with DeviceTableau(0) as e:
+        e.load(T, basis)
+        e.run_pivots(20, rule="bland")
+        e.sync()
+        t0 = time.perf_counter()
+        e.run_pivots(k, rule="bland")
+        e.sync()
+        gpu_s = time.perf_counter() - t0
+        st, it, z = e.state()
+        hist = e.history().tolist()
+    Tc, bc = T.copy(), basis.copy()
+    t0 = time.perf_counter()
+    stc, hc = C.solve(Tc, bc, rule="bland", max_iters=k_cpu)
+    cpu_s = time.perf_counter() - t0
+    return {"config": "5: degenerate 4096x4096 LP, Bland", "gpu_pivots": k,
+            "gpu_pivots_per_s": k / gpu_s, "status_after": st, "iters": it,
+            "cpu_oracle_pivots_per_s": len(hc) / cpu_s, "cpu_threads": C.threads(),
+            "first_pivots_match_oracle": [tuple(x) for x in hist[:len(hc)]] == hc}
+
+
+if __name__ == "__main__":
+    for fn in (config2, config5):
+        print(json.dumps(fn()), flush=True)
