@@ -28,6 +28,7 @@ sys.path.insert(0, ROOT)
 import numpy as np  # noqa: E402
 
 METRIC = "pivots/sec + row-elim HBM GB/s (% roofline), fp64 dense tableau, 1/2/4/8 GPU"
+DEFAULT_WINDOW = 0
 HBM_PEAK_GBPS = 8000.0  # MI355X spec HBM3E peak (MI355X_MICROARCH.md)
 
 
@@ -50,6 +51,9 @@ def parse():
                     help="1: the timed region replays one hipGraph with an event pair "
                          "captured around every elimination; 0: direct launches + events")
     ap.add_argument("--ld-pad", type=int, default=-1, help="column padding (doubles)")
+    ap.add_argument("--window", type=int, default=-1,
+                    help="windowed elimination: K pivots per tableau pass (0 = off, "
+                         "-1 = default: %d on one GPU, off when sharded)" % DEFAULT_WINDOW)
     ap.add_argument("--time-every", type=int, default=8,
                     help="HIP events around every k-th elimination of the timed region")
     ap.add_argument("--cpu-seconds", type=float, default=15.0,
@@ -154,6 +158,10 @@ def main():
         eng.set_ld_pad(args.ld_pad)
     row0, row1 = row_partition(m, world, rank)
     Tf, obj, basis = synth.tableau_rows("dense", m, n, args.seed, row0, row1, order="F")
+    K = args.window if args.window >= 0 else (DEFAULT_WINDOW if world == 1 else 0)
+    K = 0 if K <= 1 else K
+    if K:
+        eng.set_window(K)
     eng.load_rows(Tf, obj, basis, m, row0)
     del Tf
     if args.nt >= 0 or args.ilv >= 0 or args.R or args.wgs:
@@ -173,7 +181,7 @@ def main():
     barrier()
     eng.sync()
     t0 = time.perf_counter()
-    eng.run_pivots(args.steps, time_elim=args.time_every, **opts)
+    eng.run_pivots(args.steps, time_elim=1 if K else args.time_every, **opts)
     eng.sync()
     t1 = time.perf_counter()
     barrier()
@@ -186,22 +194,33 @@ def main():
     if status != 4 or iters != args.warmup + args.steps:
         raise SystemExit(f"pivot loop ended early: status {status}, iters {iters}")
     ms_tot, launches, touched = eng.elim_timing(reset=True)
-    window = (f"timed region: HIP event-record nodes around every {args.time_every}th "
-              f"elimination inside the replayed hipGraph, on the engine stream" if use_graph else
-              f"timed region: HIP events around every {args.time_every}th elimination launch")
+    what = "flush (window pass)" if K else "elimination"
+    every = "every" if K else f"every {args.time_every}th"
+    window = (f"timed region: HIP event-record nodes around {every} {what} inside the "
+              f"replayed hipGraph, on the engine stream" if use_graph else
+              f"timed region: HIP events around {every} {what} launch")
     avg_ms = ms_tot / launches
     m_local = row1 - row0
     N = n + m + 1
-    cols_per_launch = touched / args.steps  # touched_total counts every pivot
-    # algorithmic HBM bytes of one elimination launch: read+write 16 B for every
-    # touched element except the entering column, which is only written (8 B)
-    alg_bytes = 16.0 * m_local * (cols_per_launch - 1.0) + 8.0 * m_local
+    if K:
+        # one flush per window; touched_total counts each flush's column list
+        flushes = -(-args.steps // K)
+        cols_per_launch = touched / flushes
+        k_eff = args.steps / flushes
+        # read+write 16 B per listed element, plus the window's pivot columns
+        # f_s (m) and pivot-row values p_s (listed columns)
+        alg_bytes = 16.0 * m_local * cols_per_launch + 8.0 * k_eff * (m_local + cols_per_launch)
+    else:
+        cols_per_launch = touched / args.steps  # touched_total counts every pivot
+        # algorithmic HBM bytes of one elimination launch: read+write 16 B for every
+        # touched element except the entering column, which is only written (8 B)
+        alg_bytes = 16.0 * m_local * (cols_per_launch - 1.0) + 8.0 * m_local
     dense_bytes = 16.0 * (m_local + 1) * N  # SURVEY §8(d) per-pivot figure (no skip)
     achieved = alg_bytes / (avg_ms * 1e-3) / 1e9
     traffic = None
     try:
         tj = json.load(open(args.traffic_json))
-        key = f"{m}x{n}_w{world}_{'dense' if args.dense else 'skip'}"
+        key = f"{m}x{n}_w{world}_{'dense' if args.dense else 'skip'}" + (f"_k{K}" if K else "")
         traffic = tj.get(key, {}).get("hbm_bytes_per_launch")
     except (OSError, ValueError):
         pass
@@ -232,10 +251,12 @@ def main():
                        "elimination": "dense sweep" if args.dense else "skip p[j]==0 columns",
                        "timing": "hipGraph replay" if use_graph else "direct launches",
                        "elim_variant": eng.elim_variant(),
+                       "window": K,
                        "parallelism": f"row-shard x{world}" if world > 1 else "single GPU"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBPS,
-                         "traffic": traffic, "kernel": "spx::elim_kernel",
+                         "traffic": traffic,
+                         "kernel": "spx::flush_kernel" if K else "spx::elim_kernel",
                          "avg_launch_us": avg_ms * 1e3,
                          "alg_bytes_per_launch": alg_bytes,
                          "touched_cols_per_launch": cols_per_launch,

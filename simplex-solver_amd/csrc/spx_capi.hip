@@ -30,6 +30,7 @@
 
 #include "../../include/spx.h"
 #include "spx_kernels.hpp"
+#include "spx_delayed.hpp"
 
 using namespace spx;
 
@@ -114,6 +115,10 @@ struct spx_ctx {
   int tune_R = 0;          // 0: automatic
   int tune_wgs = 0;        // 0: automatic (2048)
 
+  // windowed (delayed) elimination: 0 = off (fused per-pivot elimination)
+  int win_k = 0;
+  Window win{};
+
   // graph cache
   hipGraphExec_t gexec = nullptr;
   int gchunk = 0;
@@ -121,6 +126,7 @@ struct spx_ctx {
   int64_t tpivots = 0;
   size_t tev0 = 0;                  // first event index the timed graph records
   int tevery = 0;                   // its sampling period
+  size_t tev_n = 0;                 // event pairs it records
 
   // elimination timing
   std::vector<std::pair<hipEvent_t, hipEvent_t>> ev;
@@ -183,6 +189,14 @@ int free_buffers(spx_ctx* ctx) {
   dfree(ctx->ratio_part);
   dfree(ctx->sendbuf);
   dfree(ctx->recvbuf);
+  dfree(ctx->win.F);
+  dfree(ctx->win.P);
+  dfree(ctx->win.r);
+  dfree(ctx->win.c);
+  dfree(ctx->win.made);
+  dfree(ctx->win.touched);
+  dfree(ctx->win.list);
+  dfree(ctx->win.count);
   ctx->loaded = false;
   return SPX_OK;
 }
@@ -314,6 +328,63 @@ int record_event(spx_ctx* ctx, hipEvent_t ev) {
   return SPX_OK;
 }
 
+template <int R, int KMAX>
+void launch_flush_t(spx_ctx* ctx, int npiv) {
+  const bool nts = (ctx->elim_nt & 2) != 0;
+  if (nts)
+    hipLaunchKernelGGL((flush_kernel<R, KMAX, true>), dim3(ctx->rch * ctx->G), dim3(BLK), 0,
+                       ctx->stream, ctx->A, ctx->ld, ctx->m_local, ctx->row0, ctx->N, ctx->win,
+                       npiv, ctx->rch, ctx->G, ctx->prm, ctx->st);
+  else
+    hipLaunchKernelGGL((flush_kernel<R, KMAX, false>), dim3(ctx->rch * ctx->G), dim3(BLK), 0,
+                       ctx->stream, ctx->A, ctx->ld, ctx->m_local, ctx->row0, ctx->N, ctx->win,
+                       npiv, ctx->rch, ctx->G, ctx->prm, ctx->st);
+}
+
+void launch_flush(spx_ctx* ctx, int npiv) {
+  const int K = ctx->win_k;
+  if (ctx->R >= 4) {
+    if (K <= 4) launch_flush_t<4, 4>(ctx, npiv);
+    else if (K <= 8) launch_flush_t<4, 8>(ctx, npiv);
+    else launch_flush_t<4, 16>(ctx, npiv);
+  } else {
+    if (K <= 4) launch_flush_t<2, 4>(ctx, npiv);
+    else if (K <= 8) launch_flush_t<2, 8>(ctx, npiv);
+    else launch_flush_t<2, 16>(ctx, npiv);
+  }
+}
+
+// Enqueue one window of npiv (<= win_k) pivots followed by its flush.
+int enqueue_window(spx_ctx* ctx, int npiv, bool time_flush) {
+  for (int q = 0; q < npiv; ++q) {
+    hipLaunchKernelGGL(lazy_ratio_kernel, dim3(ctx->nbr), dim3(BLK), 0, ctx->stream, ctx->A,
+                       ctx->ld, ctx->m_local, ctx->row0, ctx->N, ctx->obj, ctx->win, q,
+                       ctx->enter_part, ctx->nbn, ctx->ratio_part, ctx->basis, ctx->prm,
+                       ctx->st);
+    hipLaunchKernelGGL(lazy_norm_kernel, dim3(ctx->nbn), dim3(BLK), 0, ctx->stream, ctx->A,
+                       ctx->ld, ctx->m_local, ctx->row0, ctx->N, ctx->obj, ctx->win, q,
+                       ctx->ratio_part, ctx->enter_part, ctx->basis, ctx->hist, ctx->prm,
+                       ctx->st);
+  }
+  if (time_flush) {
+    if (ctx->ev_used == ctx->ev.size()) {
+      hipEvent_t a, b;
+      HIPC(hipEventCreate(&a));
+      HIPC(hipEventCreate(&b));
+      ctx->ev.emplace_back(a, b);
+    }
+    auto& e = ctx->ev[ctx->ev_used++];
+    int rc = record_event(ctx, e.first);
+    if (rc) return rc;
+    launch_flush(ctx, npiv);
+    if ((rc = record_event(ctx, e.second))) return rc;
+  } else {
+    launch_flush(ctx, npiv);
+  }
+  HIPC(hipGetLastError());
+  return SPX_OK;
+}
+
 // Enqueue one pivot (all launches on ctx->stream; no host synchronisation).
 int enqueue_pivot(spx_ctx* ctx, bool time_elim) {
   if (!ctx->sharded) {
@@ -342,6 +413,18 @@ int enqueue_pivot(spx_ctx* ctx, bool time_elim) {
     launch_elim(ctx);
   }
   HIPC(hipGetLastError());
+  return SPX_OK;
+}
+
+// npiv pivots in the context's mode: one window (<= win_k pivots) + its flush,
+// or npiv fused single-pivot steps.  `time_k` > 0 brackets eliminations (or
+// the flush) with events: every time_k-th elimination / every flush.
+int enqueue_pivots(spx_ctx* ctx, int npiv, int time_k, int64_t first = 0) {
+  if (ctx->win_k) return enqueue_window(ctx, npiv, time_k > 0);
+  for (int i = 0; i < npiv; ++i) {
+    const int rc = enqueue_pivot(ctx, time_k > 0 && (first + i) % time_k == 0);
+    if (rc) return rc;
+  }
   return SPX_OK;
 }
 
@@ -390,7 +473,7 @@ int begin_call(spx_ctx* ctx, const spx_opts* o, int64_t fc = -1, int64_t fr = -1
   if ((rc = write_params(ctx, o))) return rc;
   if ((rc = set_state_fields(ctx, ST_RUNNING, fc, fr))) return rc;
   launch_norm<MODE_INIT>(ctx);
-  launch_prime(ctx);
+  if (!ctx->win_k) launch_prime(ctx);  // a window's first lazy_ratio primes itself
   HIPC(hipGetLastError());
   return SPX_OK;
 }
@@ -401,8 +484,7 @@ int build_graph(spx_ctx* ctx, int chunk) {
   ctx->gexec = nullptr;
   hipGraph_t g = nullptr;
   HIPC(hipStreamBeginCapture(ctx->stream, hipStreamCaptureModeThreadLocal));
-  int rc = SPX_OK;
-  for (int i = 0; i < chunk && rc == SPX_OK; ++i) rc = enqueue_pivot(ctx, false);
+  int rc = enqueue_pivots(ctx, chunk, 0);
   hipError_t e = hipStreamEndCapture(ctx->stream, &g);
   if (rc) {
     if (g) (void)hipGraphDestroy(g);
@@ -452,6 +534,21 @@ int alloc_common(spx_ctx* ctx, int64_t m_local, int64_t N, int64_t m_global, int
   HIPC(hipMalloc(&ctx->hist, sizeof(int64_t) * 2 * ctx->hist_cap));
   HIPC(hipMalloc(&ctx->enter_part, sizeof(Key) * ctx->nbn));
   HIPC(hipMalloc(&ctx->ratio_part, sizeof(Key) * std::max(ctx->nbr, ctx->rch)));
+  {
+    constexpr int KW = 16;  // window capacity (largest flush_kernel instance)
+    HIPC(hipMalloc(&ctx->win.F, sizeof(double) * KW * ctx->ld));
+    HIPC(hipMalloc(&ctx->win.P, sizeof(double) * KW * N));
+    HIPC(hipMalloc(&ctx->win.r, sizeof(int64_t) * KW));
+    HIPC(hipMalloc(&ctx->win.c, sizeof(int64_t) * KW));
+    HIPC(hipMalloc(&ctx->win.made, sizeof(int32_t) * KW));
+    HIPC(hipMalloc(&ctx->win.touched, N));
+    HIPC(hipMalloc(&ctx->win.list, sizeof(int) * N));
+    HIPC(hipMalloc(&ctx->win.count, sizeof(int)));
+    HIPC(hipMemsetAsync(ctx->win.F, 0, sizeof(double) * KW * ctx->ld, ctx->stream));
+    HIPC(hipMemsetAsync(ctx->win.made, 0, sizeof(int32_t) * KW, ctx->stream));
+    HIPC(hipMemsetAsync(ctx->win.touched, 0, N, ctx->stream));
+    HIPC(hipMemsetAsync(ctx->win.count, 0, sizeof(int), ctx->stream));
+  }
   if (ctx->sharded) {
     ctx->gstride = round_up(PAYLOAD_HDR + (int64_t)sizeof(double) * N, 256);
     HIPC(hipMalloc(&ctx->sendbuf, ctx->gstride));
@@ -751,7 +848,7 @@ int spx_solve(spx_ctx* ctx, const spx_opts* opts, spx_result* res) {
   int rc = begin_call(ctx, o);
   if (rc) return rc;
   const int64_t it0 = ctx->h_st->iters;
-  const int chunk = o->chunk > 0 ? o->chunk : 32;
+  const int chunk = ctx->win_k ? ctx->win_k : (o->chunk > 0 ? o->chunk : 32);
   const bool use_graph = o->use_graph != 0 && !ctx->loop;
   if (use_graph) {
     rc = build_graph(ctx, chunk);
@@ -761,9 +858,8 @@ int spx_solve(spx_ctx* ctx, const spx_opts* opts, spx_result* res) {
   for (;;) {
     if (use_graph) {
       HIPC(hipGraphLaunch(ctx->gexec, ctx->stream));
-    } else {
-      for (int i = 0; i < chunk; ++i)
-        if ((rc = enqueue_pivot(ctx, false))) return rc;
+    } else if ((rc = enqueue_pivots(ctx, chunk, 0))) {
+      return rc;
     }
     if ((rc = pull_state(ctx))) return rc;
     status = map_status(ctx->h_st->status);
@@ -795,7 +891,7 @@ int spx_pivot(spx_ctx* ctx, const spx_opts* opts, int64_t* r, int64_t* c) {
   int rc = begin_call(ctx, opts);
   if (rc) return rc;
   const int64_t it0 = ctx->h_st->iters;
-  if ((rc = enqueue_pivot(ctx, false))) return rc;
+  if ((rc = enqueue_pivots(ctx, 1, 0))) return rc;
   if ((rc = pull_state(ctx))) return rc;
   const int status = map_status(ctx->h_st->status);
   if (status == SPX_RUNNING && ctx->h_st->iters == it0 + 1) {
@@ -814,7 +910,7 @@ int spx_pivot_at(spx_ctx* ctx, int64_t r, int64_t c) {
             "pivot position out of range");
   int rc = begin_call(ctx, nullptr, c, r);
   if (rc) return rc;
-  if ((rc = enqueue_pivot(ctx, false))) return rc;
+  if ((rc = enqueue_pivots(ctx, 1, 0))) return rc;
   // pull the post-pivot state before writing the forced fields back
   if ((rc = pull_state(ctx))) return rc;
   const int32_t st_after = ctx->h_st->status;
@@ -832,9 +928,21 @@ int spx_run_pivots(spx_ctx* ctx, const spx_opts* opts, int64_t npivots, int time
   int rc = begin_call(ctx, o);
   if (rc) return rc;
   const bool graph = o->use_graph && !ctx->loop;
+  const int unit = ctx->win_k ? ctx->win_k : 1;  // pivots per enqueue unit
+  // the whole request as a sequence of units: full windows, then a remainder
+  auto enqueue_all = [&](int tk) -> int {
+    int64_t done = 0;
+    while (done < npivots) {
+      const int n = (int)std::min<int64_t>(ctx->win_k ? unit : 1, npivots - done);
+      const int r = enqueue_pivots(ctx, n, tk, done);
+      if (r) return r;
+      done += n;
+    }
+    return SPX_OK;
+  };
   if (time_elim && graph) {
-    // one graph of exactly npivots pivots with an event pair around every
-    // elimination; instantiated before it is launched (outside any timing)
+    // one graph of exactly npivots pivots with event pairs inside; instantiated
+    // before it is launched (outside any timing)
     if (ctx->texec && (ctx->tpivots != npivots || ctx->tev0 != ctx->ev_used ||
                        ctx->tevery != time_elim)) {
       (void)hipGraphExecDestroy(ctx->texec);
@@ -844,11 +952,11 @@ int spx_run_pivots(spx_ctx* ctx, const spx_opts* opts, int64_t npivots, int time
       const size_t ev0 = ctx->ev_used;
       hipGraph_t g = nullptr;
       HIPC(hipStreamBeginCapture(ctx->stream, hipStreamCaptureModeThreadLocal));
-      for (int64_t i = 0; i < npivots && rc == SPX_OK; ++i)
-        rc = enqueue_pivot(ctx, i % time_elim == 0);
+      rc = enqueue_all(time_elim);
       hipError_t e = hipStreamEndCapture(ctx->stream, &g);
       if (rc == SPX_OK && e == hipSuccess) e = hipGraphInstantiate(&ctx->texec, g, nullptr, nullptr, 0);
       if (g) (void)hipGraphDestroy(g);
+      ctx->tev_n = ctx->ev_used - ev0;
       ctx->ev_used = ev0;  // the launch below re-records the same events
       if (rc) return rc;
       if (e != hipSuccess) {
@@ -860,21 +968,28 @@ int spx_run_pivots(spx_ctx* ctx, const spx_opts* opts, int64_t npivots, int time
       ctx->tev0 = ev0;
       ctx->tevery = time_elim;
     }
-    ctx->ev_used += (size_t)((npivots + time_elim - 1) / time_elim);
+    ctx->ev_used += ctx->tev_n;
     HIPC(hipGraphLaunch(ctx->texec, ctx->stream));
     return SPX_OK;
   }
   if (!time_elim && graph) {
-    const int chunk = o->chunk > 0 ? o->chunk : 32;
+    const int chunk = ctx->win_k ? ctx->win_k : (o->chunk > 0 ? o->chunk : 32);
     if ((rc = build_graph(ctx, chunk))) return rc;
     int64_t left = npivots;
     for (; left >= chunk; left -= chunk) HIPC(hipGraphLaunch(ctx->gexec, ctx->stream));
-    for (; left > 0; --left)
-      if ((rc = enqueue_pivot(ctx, false))) return rc;
-  } else {
-    for (int64_t i = 0; i < npivots; ++i)
-      if ((rc = enqueue_pivot(ctx, time_elim > 0 && i % time_elim == 0))) return rc;
+    if (left > 0) return enqueue_pivots(ctx, (int)left, 0);
+    return SPX_OK;
   }
+  return enqueue_all(time_elim);
+}
+
+// Windowed (delayed) elimination: K pivots per tableau pass (2..16), 0/1 = off.
+int spx_set_window(spx_ctx* ctx, int K) {
+  if (!ctx) return SPX_E_ARG;
+  CHECK_ARG(K >= 0 && K <= 16, "window must be 0..16");
+  CHECK_ARG(K <= 1 || !ctx->sharded, "windowed elimination is single-GPU only");
+  ctx->win_k = K <= 1 ? 0 : K;
+  drop_graphs(ctx);
   return SPX_OK;
 }
 

@@ -97,6 +97,7 @@ SIGNATURES = {
     "spx_state": (ctypes.c_int, [_P, ctypes.POINTER(_I32), _LP, _DP]),
     "spx_elim_timing": (ctypes.c_int, [_P, _DP, _LP, _LP, ctypes.c_int]),
     "spx_set_ld_pad": (ctypes.c_int, [_P, ctypes.c_int]),
+    "spx_set_window": (ctypes.c_int, [_P, ctypes.c_int]),
     "spx_get_elim_variant": (ctypes.c_int, [_P, _LP]),
     "spx_set_elim_variant": (ctypes.c_int, [_P, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                             ctypes.c_int]),

@@ -271,6 +271,10 @@ class DeviceTableau:
         keys = ("R", "row_chunks", "col_groups", "nt_flags", "interleave", "pipeline", "ld")
         return {k: int(v) for k, v in zip(keys, out)}
 
+    def set_window(self, K: int) -> None:
+        """Windowed elimination: K pivots per pass over the tableau (0/1 = off)."""
+        self._check(self._lib.spx_set_window(self._ctx, int(K)), "spx_set_window")
+
     def set_ld_pad(self, pad: int) -> None:
         """Extra doubles per stored column, applied at the next load."""
         self._check(self._lib.spx_set_ld_pad(self._ctx, int(pad)), "spx_set_ld_pad")
