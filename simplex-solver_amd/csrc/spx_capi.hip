@@ -111,6 +111,8 @@ struct spx_ctx {
   int elim_ilv = 1;        // interleaved column assignment
   int elim_pipe = 1;       // software-pipelined column pairs (+12% on config 3)
   int elim_xcd = 0;        // XCD-aware block swizzle
+  int flush_bpc[5] = {};   // resident flush blocks per CU, by window 2/4/8/16/32; 0 unknown
+  int n_cu = 0;
   int ld_pad = -1;         // extra doubles per column (-1: auto, 256 for big shards)
   int tune_R = 0;          // 0: automatic
   int tune_wgs = 0;        // 0: automatic (2048)
@@ -194,9 +196,8 @@ int free_buffers(spx_ctx* ctx) {
   dfree(ctx->win.r);
   dfree(ctx->win.c);
   dfree(ctx->win.made);
-  dfree(ctx->win.touched);
-  dfree(ctx->win.list);
-  dfree(ctx->win.count);
+  dfree(ctx->win.tag);
+  dfree(ctx->win.epoch);
   ctx->loaded = false;
   return SPX_OK;
 }
@@ -328,44 +329,45 @@ int record_event(spx_ctx* ctx, hipEvent_t ev) {
   return SPX_OK;
 }
 
-template <int R, int KMAX>
-void launch_flush_t(spx_ctx* ctx, int npiv) {
-  const bool nts = (ctx->elim_nt & 2) != 0;
-  if (nts)
-    hipLaunchKernelGGL((flush_kernel<R, KMAX, true>), dim3(ctx->rch * ctx->G), dim3(BLK), 0,
-                       ctx->stream, ctx->A, ctx->ld, ctx->m_local, ctx->row0, ctx->N, ctx->win,
-                       npiv, ctx->rch, ctx->G, ctx->prm, ctx->st);
-  else
-    hipLaunchKernelGGL((flush_kernel<R, KMAX, false>), dim3(ctx->rch * ctx->G), dim3(BLK), 0,
-                       ctx->stream, ctx->A, ctx->ld, ctx->m_local, ctx->row0, ctx->N, ctx->win,
-                       npiv, ctx->rch, ctx->G, ctx->prm, ctx->st);
+// ratio partial slots: prime / fused elim / lazy_ratio grids
+int ratio_part_len(const spx_ctx* ctx) {
+  return std::max({ctx->nbr, ctx->rch, NWAVE * (int)((ctx->m_local + BLK - 1) / BLK)});
 }
 
-void launch_flush(spx_ctx* ctx, int npiv) {
-  const int K = ctx->win_k;
-  if (ctx->R >= 4) {
-    if (K <= 4) launch_flush_t<4, 4>(ctx, npiv);
-    else if (K <= 8) launch_flush_t<4, 8>(ctx, npiv);
-    else launch_flush_t<4, 16>(ctx, npiv);
-  } else {
-    if (K <= 4) launch_flush_t<2, 4>(ctx, npiv);
-    else if (K <= 8) launch_flush_t<2, 8>(ctx, npiv);
-    else launch_flush_t<2, 16>(ctx, npiv);
+// flush grid: row chunks of 2*BLK rows x column groups (about target_wgs blocks)
+int flush_rch(const spx_ctx* ctx) { return (int)((ctx->m_local + 2 * BLK - 1) / (2 * BLK)); }
+// column groups: fill the resident capacity (blocks/CU x CUs) once, no tail wave
+int flush_groups(spx_ctx* ctx, int slot, const void* kern) {
+  if (ctx->tune_wgs > 0) return std::max(1, ctx->tune_wgs / flush_rch(ctx));
+  if (!ctx->n_cu) {
+    (void)hipDeviceGetAttribute(&ctx->n_cu, hipDeviceAttributeMultiprocessorCount, ctx->device);
+    if (ctx->n_cu <= 0) ctx->n_cu = 256;
   }
+  if (!ctx->flush_bpc[slot]) {
+    int nb = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kern, BLK, 0) != hipSuccess || nb < 1)
+      nb = 2;
+    ctx->flush_bpc[slot] = nb;
+  }
+  return std::max(1, ctx->flush_bpc[slot] * ctx->n_cu / flush_rch(ctx));
 }
+// lazy_ratio grid: one row per thread
+int lazy_ratio_grid(const spx_ctx* ctx) { return (int)((ctx->m_local + BLK - 1) / BLK); }
 
-// Enqueue one window of npiv (<= win_k) pivots followed by its flush.
-int enqueue_window(spx_ctx* ctx, int npiv, bool time_flush) {
+template <int KMAX>
+int enqueue_window_t(spx_ctx* ctx, int npiv, bool time_flush) {
+  const int nbw = lazy_ratio_grid(ctx);
   for (int q = 0; q < npiv; ++q) {
-    hipLaunchKernelGGL(lazy_ratio_kernel, dim3(ctx->nbr), dim3(BLK), 0, ctx->stream, ctx->A,
+    hipLaunchKernelGGL(lazy_ratio_kernel<KMAX>, dim3(nbw), dim3(BLK), 0, ctx->stream, ctx->A,
                        ctx->ld, ctx->m_local, ctx->row0, ctx->N, ctx->obj, ctx->win, q,
-                       ctx->enter_part, ctx->nbn, ctx->ratio_part, ctx->basis, ctx->prm,
-                       ctx->st);
-    hipLaunchKernelGGL(lazy_norm_kernel, dim3(ctx->nbn), dim3(BLK), 0, ctx->stream, ctx->A,
-                       ctx->ld, ctx->m_local, ctx->row0, ctx->N, ctx->obj, ctx->win, q,
-                       ctx->ratio_part, ctx->enter_part, ctx->basis, ctx->hist, ctx->prm,
-                       ctx->st);
+                       ctx->enter_part, NWAVE * ctx->nbn, ctx->ratio_part, ctx->basis,
+                       ctx->prm, ctx->st);
+    hipLaunchKernelGGL(lazy_norm_kernel<KMAX>, dim3(ctx->nbn), dim3(BLK), 0, ctx->stream,
+                       ctx->A, ctx->ld, ctx->m_local, ctx->row0, ctx->N, ctx->obj, ctx->win, q,
+                       ctx->ratio_part, NWAVE * nbw, ctx->enter_part, ctx->basis, ctx->hist,
+                       ctx->prm, ctx->st);
   }
+  std::pair<hipEvent_t, hipEvent_t>* e = nullptr;
   if (time_flush) {
     if (ctx->ev_used == ctx->ev.size()) {
       hipEvent_t a, b;
@@ -373,16 +375,40 @@ int enqueue_window(spx_ctx* ctx, int npiv, bool time_flush) {
       HIPC(hipEventCreate(&b));
       ctx->ev.emplace_back(a, b);
     }
-    auto& e = ctx->ev[ctx->ev_used++];
-    int rc = record_event(ctx, e.first);
+    e = &ctx->ev[ctx->ev_used++];
+    const int rc = record_event(ctx, e->first);
     if (rc) return rc;
-    launch_flush(ctx, npiv);
-    if ((rc = record_event(ctx, e.second))) return rc;
-  } else {
-    launch_flush(ctx, npiv);
   }
+  const int rch = flush_rch(ctx);
+  const int slot = KMAX == 2 ? 0 : KMAX == 4 ? 1 : KMAX == 8 ? 2 : KMAX == 16 ? 3 : 4;
+  auto go = [&](auto kern) {
+    const int G = flush_groups(ctx, slot, (const void*)kern);
+    hipLaunchKernelGGL(kern, dim3(rch * G), dim3(BLK), 0, ctx->stream, ctx->A, ctx->ld,
+                       ctx->m_local, ctx->row0, ctx->N, ctx->win, npiv, rch, G, ctx->prm,
+                       ctx->st);
+  };
+  if (ctx->elim_nt & 2) go(flush_kernel<KMAX, true>);
+  else go(flush_kernel<KMAX, false>);
+  if (e) {
+    const int rc = record_event(ctx, e->second);
+    if (rc) return rc;
+  }
+  if (npiv == KMAX)  // full windows leave the fast-path columns' leaving rows to it
+    hipLaunchKernelGGL(row_fix_kernel<KMAX>, dim3(ctx->nbn), dim3(BLK), 0, ctx->stream, ctx->A,
+                       ctx->ld, ctx->row0, ctx->N, ctx->win);
   HIPC(hipGetLastError());
   return SPX_OK;
+}
+
+// Enqueue one window of npiv (<= win_k) pivots followed by its flush.
+int enqueue_window(spx_ctx* ctx, int npiv, bool time_flush) {
+  switch (ctx->win_k) {
+    case 2: return enqueue_window_t<2>(ctx, npiv, time_flush);
+    case 4: return enqueue_window_t<4>(ctx, npiv, time_flush);
+    case 8: return enqueue_window_t<8>(ctx, npiv, time_flush);
+    case 16: return enqueue_window_t<16>(ctx, npiv, time_flush);
+    default: return enqueue_window_t<32>(ctx, npiv, time_flush);
+  }
 }
 
 // Enqueue one pivot (all launches on ctx->stream; no host synchronisation).
@@ -473,7 +499,13 @@ int begin_call(spx_ctx* ctx, const spx_opts* o, int64_t fc = -1, int64_t fr = -1
   if ((rc = write_params(ctx, o))) return rc;
   if ((rc = set_state_fields(ctx, ST_RUNNING, fc, fr))) return rc;
   launch_norm<MODE_INIT>(ctx);
-  if (!ctx->win_k) launch_prime(ctx);  // a window's first lazy_ratio primes itself
+  if (!ctx->win_k) {
+    launch_prime(ctx);
+  } else {  // lazy_ratio reduces NWAVE*nbn per-wave partials; INIT wrote the first nbn
+    const int n = (NWAVE - 1) * ctx->nbn;
+    hipLaunchKernelGGL(fill_none_kernel, dim3((n + BLK - 1) / BLK), dim3(BLK), 0, ctx->stream,
+                       ctx->enter_part + ctx->nbn, n);
+  }
   HIPC(hipGetLastError());
   return SPX_OK;
 }
@@ -532,22 +564,21 @@ int alloc_common(spx_ctx* ctx, int64_t m_local, int64_t N, int64_t m_global, int
   HIPC(hipMalloc(&ctx->list, sizeof(int) * N));
   HIPC(hipMalloc(&ctx->basis, sizeof(int64_t) * std::max<int64_t>(1, m_global)));
   HIPC(hipMalloc(&ctx->hist, sizeof(int64_t) * 2 * ctx->hist_cap));
-  HIPC(hipMalloc(&ctx->enter_part, sizeof(Key) * ctx->nbn));
-  HIPC(hipMalloc(&ctx->ratio_part, sizeof(Key) * std::max(ctx->nbr, ctx->rch)));
+  HIPC(hipMalloc(&ctx->enter_part, sizeof(Key) * NWAVE * ctx->nbn));  // per wave (windows)
+  HIPC(hipMalloc(&ctx->ratio_part, sizeof(Key) * ratio_part_len(ctx)));
   {
-    constexpr int KW = 16;  // window capacity (largest flush_kernel instance)
     HIPC(hipMalloc(&ctx->win.F, sizeof(double) * KW * ctx->ld));
     HIPC(hipMalloc(&ctx->win.P, sizeof(double) * KW * N));
     HIPC(hipMalloc(&ctx->win.r, sizeof(int64_t) * KW));
     HIPC(hipMalloc(&ctx->win.c, sizeof(int64_t) * KW));
     HIPC(hipMalloc(&ctx->win.made, sizeof(int32_t) * KW));
-    HIPC(hipMalloc(&ctx->win.touched, N));
-    HIPC(hipMalloc(&ctx->win.list, sizeof(int) * N));
-    HIPC(hipMalloc(&ctx->win.count, sizeof(int)));
+    HIPC(hipMalloc(&ctx->win.tag, sizeof(uint32_t) * N));
+    HIPC(hipMalloc(&ctx->win.epoch, sizeof(uint32_t)));
     HIPC(hipMemsetAsync(ctx->win.F, 0, sizeof(double) * KW * ctx->ld, ctx->stream));
+    HIPC(hipMemsetAsync(ctx->win.P, 0, sizeof(double) * KW * N, ctx->stream));
     HIPC(hipMemsetAsync(ctx->win.made, 0, sizeof(int32_t) * KW, ctx->stream));
-    HIPC(hipMemsetAsync(ctx->win.touched, 0, N, ctx->stream));
-    HIPC(hipMemsetAsync(ctx->win.count, 0, sizeof(int), ctx->stream));
+    HIPC(hipMemsetAsync(ctx->win.tag, 0, sizeof(uint32_t) * N, ctx->stream));
+    HIPC(hipMemsetAsync(ctx->win.epoch, 0, sizeof(uint32_t), ctx->stream));
   }
   if (ctx->sharded) {
     ctx->gstride = round_up(PAYLOAD_HDR + (int64_t)sizeof(double) * N, 256);
@@ -986,7 +1017,8 @@ int spx_run_pivots(spx_ctx* ctx, const spx_opts* opts, int64_t npivots, int time
 // Windowed (delayed) elimination: K pivots per tableau pass (2..16), 0/1 = off.
 int spx_set_window(spx_ctx* ctx, int K) {
   if (!ctx) return SPX_E_ARG;
-  CHECK_ARG(K >= 0 && K <= 16, "window must be 0..16");
+  CHECK_ARG(K == 0 || K == 1 || K == 2 || K == 4 || K == 8 || K == 16 || K == 32,
+            "window must be 0, 1, 2, 4, 8, 16 or 32");
   CHECK_ARG(K <= 1 || !ctx->sharded, "windowed elimination is single-GPU only");
   ctx->win_k = K <= 1 ? 0 : K;
   drop_graphs(ctx);
@@ -1051,7 +1083,7 @@ int spx_set_elim_variant(spx_ctx* ctx, int R, int target_wgs, int nt_flags, int 
   if (ctx->loaded) {
     if (ctx->rch > ctx->nbr) {  // ratio_part must hold rch partials
       dfree(ctx->ratio_part);
-      HIPC(hipMalloc(&ctx->ratio_part, sizeof(Key) * std::max(ctx->nbr, ctx->rch)));
+      HIPC(hipMalloc(&ctx->ratio_part, sizeof(Key) * ratio_part_len(ctx)));
     }
   }
   drop_graphs(ctx);
