@@ -28,7 +28,7 @@ sys.path.insert(0, ROOT)
 import numpy as np  # noqa: E402
 
 METRIC = "pivots/sec + row-elim HBM GB/s (% roofline), fp64 dense tableau, 1/2/4/8 GPU"
-DEFAULT_WINDOW = 0
+DEFAULT_WINDOW = 16  # windowed elimination on one GPU
 HBM_PEAK_GBPS = 8000.0  # MI355X spec HBM3E peak (MI355X_MICROARCH.md)
 
 
@@ -47,6 +47,8 @@ def parse():
     ap.add_argument("--ilv", type=int, default=-1, help="elim interleaved columns (-1: default)")
     ap.add_argument("--R", type=int, default=0, help="elim rows per thread (0: auto)")
     ap.add_argument("--wgs", type=int, default=0, help="elim grid target (0: auto)")
+    ap.add_argument("--fv", type=int, default=-1,
+                    help="windowed flush variant 0-4 (rows/thread x ring depth; -1 default)")
     ap.add_argument("--graph", type=int, default=1,
                     help="1: the timed region replays one hipGraph with an event pair "
                          "captured around every elimination; 0: direct launches + events")
@@ -164,11 +166,11 @@ def main():
         eng.set_window(K)
     eng.load_rows(Tf, obj, basis, m, row0)
     del Tf
-    if args.nt >= 0 or args.ilv >= 0 or args.R or args.wgs:
+    if args.nt >= 0 or args.ilv >= 0 or args.R or args.wgs or args.fv >= 0:
         v = eng.elim_variant()
-        eng.set_elim_variant(args.R, args.wgs, -1 if args.nt < 0 else args.nt,
-                             (v["interleave"] | (0 if v["pipeline"] else 2)) if args.ilv < 0
-                             else args.ilv)
+        ilv = ((v["interleave"] | (0 if v["pipeline"] else 2)) if args.ilv < 0 else args.ilv)
+        ilv |= max(args.fv, 0) << 8
+        eng.set_elim_variant(args.R, args.wgs, -1 if args.nt < 0 else args.nt, ilv)
     opts = dict(rule=args.rule, skip_zero_cols=not args.dense, use_graph=use_graph, chunk=32)
 
     def barrier():

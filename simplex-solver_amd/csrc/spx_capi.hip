@@ -111,7 +111,9 @@ struct spx_ctx {
   int elim_ilv = 1;        // interleaved column assignment
   int elim_pipe = 1;       // software-pipelined column pairs (+12% on config 3)
   int elim_xcd = 0;        // XCD-aware block swizzle
-  int flush_bpc[5] = {};   // resident flush blocks per CU, by window 2/4/8/16/32; 0 unknown
+  int flush_bpc[5 * 8] = {};  // resident flush blocks per CU, by (window 2..32, variant); 0 unknown
+  int flush_var = 0;       // flush kernel variant (rows per thread x columns per step)
+  int last_flush_G = 0;    // column groups of the last flush launch
   int n_cu = 0;
   int ld_pad = -1;         // extra doubles per column (-1: auto, 256 for big shards)
   int tune_R = 0;          // 0: automatic
@@ -335,10 +337,12 @@ int ratio_part_len(const spx_ctx* ctx) {
 }
 
 // flush grid: row chunks of 2*BLK rows x column groups (about target_wgs blocks)
-int flush_rch(const spx_ctx* ctx) { return (int)((ctx->m_local + 2 * BLK - 1) / (2 * BLK)); }
+int flush_rch(const spx_ctx* ctx, int rt) {
+  return (int)((ctx->m_local + rt * BLK - 1) / (rt * BLK));
+}
 // column groups: fill the resident capacity (blocks/CU x CUs) once, no tail wave
-int flush_groups(spx_ctx* ctx, int slot, const void* kern) {
-  if (ctx->tune_wgs > 0) return std::max(1, ctx->tune_wgs / flush_rch(ctx));
+int flush_groups(spx_ctx* ctx, int slot, const void* kern, int rch) {
+  if (ctx->tune_wgs > 0) return std::max(1, ctx->tune_wgs / rch);
   if (!ctx->n_cu) {
     (void)hipDeviceGetAttribute(&ctx->n_cu, hipDeviceAttributeMultiprocessorCount, ctx->device);
     if (ctx->n_cu <= 0) ctx->n_cu = 256;
@@ -349,7 +353,7 @@ int flush_groups(spx_ctx* ctx, int slot, const void* kern) {
       nb = 2;
     ctx->flush_bpc[slot] = nb;
   }
-  return std::max(1, ctx->flush_bpc[slot] * ctx->n_cu / flush_rch(ctx));
+  return std::max(1, ctx->flush_bpc[slot] * ctx->n_cu / rch);
 }
 // lazy_ratio grid: one row per thread
 int lazy_ratio_grid(const spx_ctx* ctx) { return (int)((ctx->m_local + BLK - 1) / BLK); }
@@ -379,23 +383,34 @@ int enqueue_window_t(spx_ctx* ctx, int npiv, bool time_flush) {
     const int rc = record_event(ctx, e->first);
     if (rc) return rc;
   }
-  const int rch = flush_rch(ctx);
-  const int slot = KMAX == 2 ? 0 : KMAX == 4 ? 1 : KMAX == 8 ? 2 : KMAX == 16 ? 3 : 4;
-  auto go = [&](auto kern) {
-    const int G = flush_groups(ctx, slot, (const void*)kern);
+  const int slot = (KMAX == 2 ? 0 : KMAX == 4 ? 1 : KMAX == 8 ? 2 : KMAX == 16 ? 3 : 4) +
+                   5 * ctx->flush_var;
+  auto go = [&](auto kern, int rt) {
+    const int rch = flush_rch(ctx, rt);
+    const int G = flush_groups(ctx, slot, (const void*)kern, rch);
+    ctx->last_flush_G = G;
     hipLaunchKernelGGL(kern, dim3(rch * G), dim3(BLK), 0, ctx->stream, ctx->A, ctx->ld,
                        ctx->m_local, ctx->row0, ctx->N, ctx->win, npiv, rch, G, ctx->prm,
                        ctx->st);
   };
-  if (ctx->elim_nt & 2) go(flush_kernel<KMAX, true>);
-  else go(flush_kernel<KMAX, false>);
+  const bool nts = (ctx->elim_nt & 2) != 0;
+  // variants (rows per thread RT x register-ring depth D; A: sweep direction
+  // alternating per window): 0 2x4A (default), 1 2x4, 2 4x4, 3 4x4A, 4 2x8
+  // (profiles/r01/tune_flush_*.log)
+  switch (ctx->flush_var) {
+    case 1: nts ? go(flush_kernel<KMAX, 2, 4, true>, 2) : go(flush_kernel<KMAX, 2, 4, false>, 2); break;
+    case 2: nts ? go(flush_kernel<KMAX, 4, 4, true>, 4) : go(flush_kernel<KMAX, 4, 4, false>, 4); break;
+    case 3: nts ? go(flush_kernel<KMAX, 4, 4, true, true>, 4) : go(flush_kernel<KMAX, 4, 4, false, true>, 4); break;
+    case 4: nts ? go(flush_kernel<KMAX, 2, 8, true>, 2) : go(flush_kernel<KMAX, 2, 8, false>, 2); break;
+    default: nts ? go(flush_kernel<KMAX, 2, 4, true, true>, 2) : go(flush_kernel<KMAX, 2, 4, false, true>, 2);
+  }
   if (e) {
     const int rc = record_event(ctx, e->second);
     if (rc) return rc;
   }
   if (npiv == KMAX)  // full windows leave the fast-path columns' leaving rows to it
     hipLaunchKernelGGL(row_fix_kernel<KMAX>, dim3(ctx->nbn), dim3(BLK), 0, ctx->stream, ctx->A,
-                       ctx->ld, ctx->row0, ctx->N, ctx->win);
+                       ctx->ld, ctx->m_local, ctx->row0, ctx->N, ctx->win);
   HIPC(hipGetLastError());
   return SPX_OK;
 }
@@ -577,6 +592,8 @@ int alloc_common(spx_ctx* ctx, int64_t m_local, int64_t N, int64_t m_global, int
     HIPC(hipMemsetAsync(ctx->win.F, 0, sizeof(double) * KW * ctx->ld, ctx->stream));
     HIPC(hipMemsetAsync(ctx->win.P, 0, sizeof(double) * KW * N, ctx->stream));
     HIPC(hipMemsetAsync(ctx->win.made, 0, sizeof(int32_t) * KW, ctx->stream));
+    HIPC(hipMemsetAsync(ctx->win.r, 0, sizeof(int64_t) * KW, ctx->stream));
+    HIPC(hipMemsetAsync(ctx->win.c, 0, sizeof(int64_t) * KW, ctx->stream));
     HIPC(hipMemsetAsync(ctx->win.tag, 0, sizeof(uint32_t) * N, ctx->stream));
     HIPC(hipMemsetAsync(ctx->win.epoch, 0, sizeof(uint32_t), ctx->stream));
   }
@@ -1015,6 +1032,22 @@ int spx_run_pivots(spx_ctx* ctx, const spx_opts* opts, int64_t npivots, int time
 }
 
 // Windowed (delayed) elimination: K pivots per tableau pass (2..16), 0/1 = off.
+#ifdef SPX_PHASE_TIMING
+// diagnostic build only (tools/probe_phases.py): copy the phase timestamps
+int spx_probe_read(unsigned long long* out, int n) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(spx::spx_probe_buf),
+                             sizeof(unsigned long long) * std::min(n, 1024 + 2 * 8192)) ==
+                 hipSuccess
+             ? 0 : -1;
+}
+// flush grid of the last window (diagnostic)
+int spx_probe_flush_grid(spx_ctx* ctx, int* rch, int* G) {
+  *rch = flush_rch(ctx, ctx->flush_var == 2 || ctx->flush_var == 3 ? 4 : 2);
+  *G = ctx->last_flush_G;
+  return 0;
+}
+#endif
+
 int spx_set_window(spx_ctx* ctx, int K) {
   if (!ctx) return SPX_E_ARG;
   CHECK_ARG(K == 0 || K == 1 || K == 2 || K == 4 || K == 8 || K == 16 || K == 32,
@@ -1079,6 +1112,7 @@ int spx_set_elim_variant(spx_ctx* ctx, int R, int target_wgs, int nt_flags, int 
   ctx->elim_ilv = interleave & 1;
   ctx->elim_pipe = (interleave & 2) ? 0 : 1;  // bit 1 of `interleave`: disable pipelining
   ctx->elim_xcd = (interleave & 4) ? 1 : 0;   // bit 2: XCD-aware block swizzle
+  ctx->flush_var = (interleave >> 8) & 7;     // bits 8-10: windowed flush variant
   choose_geometry(ctx);  // also resolves the automatic nt flags
   if (ctx->loaded) {
     if (ctx->rch > ctx->nbr) {  // ratio_part must hold rch partials

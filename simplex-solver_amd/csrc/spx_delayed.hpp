@@ -32,6 +32,32 @@
 
 namespace spx {
 
+// Diagnostic phase timestamps (tools/probe_phases.py builds a separate library
+// with -DSPX_PHASE_TIMING): block 0 / thread 0 of each window kernel records
+// s_memrealtime (100 MHz) at its phase boundaries.  Compiled out otherwise.
+#ifdef SPX_PHASE_TIMING
+__device__ unsigned long long spx_probe_buf[1024 + 2 * 8192];
+// flush blocks: [1024 + 2*b] = entry, [1024 + 2*b + 1] = exit of block b
+#define SPX_PROBE_BLOCK(which)                                                               \
+  do {                                                                                       \
+    if (threadIdx.x == 0 && blockIdx.x < 8192)                                               \
+      spx_probe_buf[1024 + 2 * blockIdx.x + (which)] = __builtin_amdgcn_s_memrealtime();    \
+  } while (0)
+#define SPX_PROBE(slot, kind, phase, cond)                                                  \
+  do {                                                                                       \
+    if (blockIdx.x == 0 && threadIdx.x == 0 && (cond))                                       \
+      spx_probe_buf[(((slot) * 4 + (kind)) * 4 + (phase)) & 1023] =                          \
+          __builtin_amdgcn_s_memrealtime();                                                  \
+  } while (0)
+#else
+#define SPX_PROBE(slot, kind, phase, cond) \
+  do {                                     \
+  } while (0)
+#define SPX_PROBE_BLOCK(which) \
+  do {                         \
+  } while (0)
+#endif
+
 constexpr int KW = 32;  // window capacity: slots of F / P
 
 // column tags: the window epoch (low 30 bits) + path flags for the flush
@@ -58,6 +84,29 @@ __device__ __forceinline__ double apply_pivot(double v, int64_t il, int64_t j, i
   return (il == rl_s) ? p_sj : msub(v, f_si, p_sj);
 }
 
+// This lane's share (keys lane, lane+64, ...) of a per-wave argmin over n >= 1
+// keys: up to 8 keys per lane with every load issued before the first compare
+// (a plain strided loop waits one memory latency per key).  wave_min() after.
+__device__ __forceinline__ KeyR lane_keys(const Key* __restrict__ part, int n) {
+  KeyR k = keyr_none();
+  const int lane = threadIdx.x & 63;
+  for (int b = lane; b < n; b += 64 * 8) {
+    double v[8];
+    int64_t t[8], r[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int x = min(b + 64 * u, n - 1);
+      v[u] = part[x].v;
+      t[u] = part[x].t;
+      r[u] = part[x].row;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      if (b + 64 * u < n) kmin(k, v[u], t[u], r[u]);
+  }
+  return k;
+}
+
 // Fill n keys with "no candidate" (entering partials beyond norm<INIT>'s).
 __global__ __launch_bounds__(BLK) void fill_none_kernel(Key* __restrict__ k, int n) {
   const int x = blockIdx.x * BLK + threadIdx.x;
@@ -75,26 +124,26 @@ __global__ __launch_bounds__(BLK) void lazy_ratio_kernel(
     const double* __restrict__ obj, Window win, int q, const Key* __restrict__ enter_part,
     int n_enter_part, Key* __restrict__ ratio_part, const int64_t* __restrict__ basis,
     const Params* __restrict__ prm, State* st) {
+  SPX_PROBE(q, 0, 0, true);
   // independent loads first: state, entering partials, this row's f_s
   const int32_t status = st->status;
   const int64_t forced_c = st->forced_c;
   const int32_t rule = prm->rule;
   const double eps_piv = prm->eps_piv;
   const bool skip = prm->skip_zero != 0;
-  KeyR e = keyr_none();  // per-wave reduction: no LDS round, no block barrier
-  for (int x = threadIdx.x & 63; x < n_enter_part; x += 64)
-    kmin(e, enter_part[x].v, enter_part[x].t, enter_part[x].row);
+  KeyR e = lane_keys(enter_part, n_enter_part);  // per wave: no LDS round, no barrier
   const int64_t i = (int64_t)blockIdx.x * BLK + threadIdx.x;
   const bool live = i < m_local;
+  // slot data, loaded unconditionally (stale slots >= q are valid memory, unused)
+  // so no load waits behind a per-slot branch
   double fs[KMAX];
   int64_t rls[KMAX], cs[KMAX];
+  const int64_t ic = live ? i : 0;
 #pragma unroll
   for (int s = 0; s < KMAX; ++s) {
-    if (s < q) {
-      fs[s] = live ? win.F[(int64_t)s * ld + i] : 0.0;
-      rls[s] = win.r[s] - row0;
-      cs[s] = win.c[s];
-    }
+    fs[s] = win.F[(int64_t)s * ld + ic];
+    rls[s] = win.r[s] - row0;
+    cs[s] = win.c[s];
   }
   if (status != ST_RUNNING) return;
   int64_t c;
@@ -111,6 +160,7 @@ __global__ __launch_bounds__(BLK) void lazy_ratio_kernel(
     }
     c = e.row;
   }
+  SPX_PROBE(q, 0, 1, c >= 0);
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     st->c_next = c;
     st->zc_next = obj[c];
@@ -122,13 +172,27 @@ __global__ __launch_bounds__(BLK) void lazy_ratio_kernel(
   double bv = live ? A[rhs * ld + i] : 0.0;
   const double* __restrict__ Pc = win.P + c * KW;
   const double* __restrict__ Pb = win.P + rhs * KW;
+  // in chunks of 8 slots: the chunk's p values are loaded before its updates
 #pragma unroll
-  for (int s = 0; s < KMAX; ++s) {
-    if (s < q) {
-      fv = apply_pivot(fv, i, c, rls[s], cs[s], fs[s], Pc[s], skip);
-      bv = apply_pivot(bv, i, rhs, rls[s], cs[s], fs[s], Pb[s], skip);
+  for (int s0 = 0; s0 < KMAX; s0 += 8) {
+    if (s0 < q) {
+      double pc[8], pb[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        pc[u] = Pc[s0 + u];
+        pb[u] = Pb[s0 + u];
+      }
+#pragma unroll
+      for (int u = 0; u < 8 && s0 + u < KMAX; ++u) {
+        const int s = s0 + u;
+        if (s < q) {
+          fv = apply_pivot(fv, i, c, rls[s], cs[s], fs[s], pc[u], skip);
+          bv = apply_pivot(bv, i, rhs, rls[s], cs[s], fs[s], pb[u], skip);
+        }
+      }
     }
   }
+  SPX_PROBE(q, 0, 2, fv != 12345.678);
   KeyR k = keyr_none();
   if (live) {
     win.F[(int64_t)q * ld + i] = fv;
@@ -138,6 +202,7 @@ __global__ __launch_bounds__(BLK) void lazy_ratio_kernel(
     wave_min(k);
     if ((threadIdx.x & 63) == 0) store_key(ratio_part + blockIdx.x * NWAVE + (threadIdx.x >> 6), k);
   }
+  SPX_PROBE(q, 0, 3, true);
 }
 
 // ---------------------------------------------------------------------------
@@ -155,6 +220,7 @@ __global__ __launch_bounds__(BLK) void lazy_norm_kernel(
     int n_ratio, Key* __restrict__ enter_part, int64_t* __restrict__ basis,
     int64_t* __restrict__ hist, const Params* __restrict__ prm, State* st) {
   const bool block0 = blockIdx.x == 0 && threadIdx.x == 0;
+  SPX_PROBE(q, 1, 0, true);
   // independent loads first
   const int32_t status = st->status;
   const int64_t c = st->c_next;
@@ -167,9 +233,7 @@ __global__ __launch_bounds__(BLK) void lazy_norm_kernel(
   const int64_t n_enter = prm->n_enter;
   const int64_t iter_limit = prm->iter_limit;
   const bool skip = prm->skip_zero != 0;
-  KeyR rk = keyr_none();  // per-wave reduction of the per-wave ratio partials
-  for (int x = threadIdx.x & 63; x < n_ratio; x += 64)
-    kmin(rk, ratio_part[x].v, ratio_part[x].t, ratio_part[x].row);
+  KeyR rk = lane_keys(ratio_part, n_ratio);  // per wave, of the per-wave ratio partials
   const int64_t j = (int64_t)blockIdx.x * BLK + threadIdx.x;
   const bool live = j < N;
   double o = live ? obj[j] : 0.0;
@@ -178,12 +242,15 @@ __global__ __launch_bounds__(BLK) void lazy_norm_kernel(
   int64_t rls[KMAX], cs[KMAX];
   const double* __restrict__ Pj = win.P + (live ? j : 0) * KW;
 #pragma unroll
+  for (int s = 0; s < KMAX; s += 2) {  // unconditional: no load behind a slot branch
+    const dbl2 pp = ld2<false>(Pj + s);
+    ps[s] = pp.x;
+    ps[s + 1] = pp.y;
+  }
+#pragma unroll
   for (int s = 0; s < KMAX; ++s) {
-    if (s < q) {
-      ps[s] = Pj[s];
-      rls[s] = win.r[s] - row0;
-      cs[s] = win.c[s];
-    }
+    rls[s] = win.r[s] - row0;
+    cs[s] = win.c[s];
   }
   if (status != ST_RUNNING) {
     if (block0) win.made[q] = 0;
@@ -208,16 +275,22 @@ __global__ __launch_bounds__(BLK) void lazy_norm_kernel(
     }
     r = rk.row;
   }
+  SPX_PROBE(q, 1, 1, r >= 0);
   const int64_t rl = r - row0;
   const double piv = win.F[(int64_t)q * ld + rl];
   double v = live ? A[j * ld + rl] : 0.0;
-  double fr[KMAX];
 #pragma unroll
-  for (int s = 0; s < KMAX; ++s)
-    if (s < q) fr[s] = win.F[(int64_t)s * ld + rl];
+  for (int s0 = 0; s0 < KMAX; s0 += 8) {
+    if (s0 < q) {
+      double fr[8];
 #pragma unroll
-  for (int s = 0; s < KMAX; ++s)
-    if (s < q) v = apply_pivot(v, rl, j, rls[s], cs[s], fr[s], ps[s], skip);
+      for (int u = 0; u < 8; ++u) fr[u] = win.F[(int64_t)(s0 + u) * ld + rl];
+#pragma unroll
+      for (int u = 0; u < 8 && s0 + u < KMAX; ++u)
+        if (s0 + u < q) v = apply_pivot(v, rl, j, rls[s0 + u], cs[s0 + u], fr[u], ps[s0 + u], skip);
+    }
+  }
+  SPX_PROBE(q, 1, 2, v != 12345.678);
   KeyR ek = keyr_none();
   if (live) {
     const double p = v / piv;
@@ -262,123 +335,208 @@ __global__ __launch_bounds__(BLK) void lazy_norm_kernel(
       hist[2 * it + 1] = c;
     }
   }
+  SPX_PROBE(q, 1, 3, true);
 }
 
 // ---------------------------------------------------------------------------
-// flush_kernel<K, NTS>: apply the window's made pivots to every column tagged
-// with this window's epoch, one streaming read-modify-write pass.
-// grid = rch * G blocks: row chunk of 2*BLK rows (one dbl2 per thread) x G
-// column groups; group g owns columns g, g+G, ...  Per batch of BLK columns of
-// the group, the block compacts the tagged ones into an LDS list and stages
-// their p_s[j] in LDS; every wave then streams the list two columns at a time
-// (the next two prefetched), reading p_s[j] as LDS broadcasts.  f_s for the
-// thread's two rows stay in registers for the whole launch.
+// flush_kernel<K, RT, D, NTS>: apply the window's made pivots to every column
+// tagged with this window's epoch, one streaming read-modify-write pass.
+// grid = rch * G blocks: row chunk of RT*BLK rows x G column groups; group g
+// owns columns g, g+G, ...  Every wave walks its group's columns on its own
+// (no block barrier, no LDS): it reads 64 tags at a time (the next 64 already
+// in flight), takes the tagged columns from the ballot mask (wave-uniform),
+// keeps a ring of D columns' loads in flight, and reads p_s[j] with scalar
+// loads one column ahead, so the update is K x RT pairs of v_mul_f64 /
+// v_add_f64 with an SGPR operand -- no LDS, no readlane.  f_s of the thread's
+// rows stay in registers for the whole launch.
 // Fast path (a full window; column not SPECIAL / ZERO): the straight msub
 // chain for every row, leaving rows included -- row_fix_kernel then rewrites
 // the leaving rows of these columns.  SPECIAL (entered in this window) or ZERO
 // (skip on, some p_s[j] == 0) columns and partial windows take the exact
 // per-element path (apply_pivot), leaving rows included.
 // ---------------------------------------------------------------------------
-template <int K, bool NTS>
+// A thread's RT rows of a column: RT = 1: i0; RT = 2: (i0, i0+1); RT = 4: pairs
+// (i0, i0+1) and (i0 + 2*BLK, i0 + 2*BLK + 1), so every wave-instruction moves
+// one contiguous run.  okp[k]: pair k lies inside the local rows (the second
+// row of a pair is < ld, a multiple of 64, so it may be a padding row).
+template <int RT>
+struct Rows {
+  double v[RT];
+};
+template <int RT>
+__device__ __forceinline__ int64_t row_of(int64_t i0, int u) {
+  return i0 + (int64_t)(u >> 1) * 2 * BLK + (u & 1);
+}
+template <int RT>
+constexpr int npairs() { return RT == 1 ? 1 : RT / 2; }
+
+template <int RT, bool NT>
+__device__ __forceinline__ void ld_rows(Rows<RT>& r, const double* p, const bool* okp) {
+  if constexpr (RT == 1) {
+    if (okp[0]) r.v[0] = NT ? __builtin_nontemporal_load(p) : *p;
+  } else {
+#pragma unroll
+    for (int k = 0; k < RT / 2; ++k) {
+      if (okp[k]) {
+        const dbl2 x = ld2<NT>(p + (int64_t)k * 2 * BLK);
+        r.v[2 * k] = x.x;
+        r.v[2 * k + 1] = x.y;
+      }
+    }
+  }
+}
+
+template <int RT, bool NT>
+__device__ __forceinline__ void st_rows(double* p, const Rows<RT>& r, const bool* okp) {
+  if constexpr (RT == 1) {
+    if (okp[0]) {
+      if (NT) __builtin_nontemporal_store(r.v[0], p);
+      else *p = r.v[0];
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < RT / 2; ++k)
+      if (okp[k]) st2<NT>(p + (int64_t)k * 2 * BLK, dbl2{r.v[2 * k], r.v[2 * k + 1]});
+  }
+}
+
+struct ColCursor {  // wave-uniform walk over the tagged columns of one group
+  const uint32_t* __restrict__ tag;
+  int64_t g, G, ncol, k0;
+  uint32_t epoch, tg, tgn;
+  uint64_t mask;
+  bool rev;  // walk the group's columns in descending order
+
+  __device__ int64_t col(int64_t k) const { return g + (rev ? ncol - 1 - k : k) * G; }
+  __device__ uint32_t load(int64_t kb, int lane) const {
+    const int64_t k = kb + lane;
+    return (k < ncol) ? tag[col(k)] : 0u;
+  }
+  __device__ void start(int lane) {
+    k0 = 0;
+    tg = load(0, lane);
+    tgn = load(64, lane);
+    mask = __ballot((tg & TAG_EPOCH) == epoch && lane < ncol);
+  }
+  // next tagged column (j, flags); false when the group is exhausted
+  __device__ bool next(int64_t& j, uint32_t& fl, int lane) {
+    while (mask == 0ull) {
+      k0 += 64;
+      if (k0 >= ncol) return false;
+      tg = tgn;
+      tgn = load(k0 + 64, lane);  // the batch after, in flight
+      mask = __ballot((tg & TAG_EPOCH) == epoch && k0 + lane < ncol);
+    }
+    const int bit = __builtin_ctzll(mask);
+    mask &= mask - 1ull;
+    j = col(k0 + bit);
+    fl = (uint32_t)__builtin_amdgcn_readlane((int)tg, bit) & (TAG_SPECIAL | TAG_ZERO);
+    return true;
+  }
+};
+
+template <int K, int RT, int D, bool NTS, bool ALT = false>
 __global__ __launch_bounds__(BLK) void flush_kernel(double* __restrict__ A, int64_t ld,
                                                     int64_t m_local, int64_t row0, int64_t N,
                                                     Window win, int npiv, int rch, int G,
                                                     const Params* __restrict__ prm, State* st) {
-  constexpr int CB = 2;
-  __shared__ uint32_t list[BLK];
-  __shared__ double pls[BLK * K];
-  __shared__ int wcnt[NWAVE];
+  SPX_PROBE(K, 2, 0, true);
+  SPX_PROBE_BLOCK(0);
   int nm = 0;  // pivots made in this window: a prefix of its npiv slots
   for (int s = 0; s < npiv; ++s) nm += win.made[s];
   if (nm == 0) return;
   const bool full = nm == K;
-  const uint32_t epoch = *win.epoch & TAG_EPOCH;
   const bool skip = prm->skip_zero != 0;
   const int chunk = blockIdx.x % rch;
   const int g = blockIdx.x / rch;
   const int lane = threadIdx.x & 63;
-  const int wid = threadIdx.x >> 6;
-  const int64_t i0 = (int64_t)chunk * BLK * 2 + threadIdx.x * 2;
-  const bool ok = i0 < m_local;
-  double fx[K], fy[K];
+  const int64_t i0 = (int64_t)chunk * BLK * RT + threadIdx.x * (RT == 1 ? 1 : 2);
+  constexpr int NP = npairs<RT>();
+  bool okp[NP];
+#pragma unroll
+  for (int k = 0; k < NP; ++k) okp[k] = row_of<RT>(i0, 2 * k) < m_local;
+  double f[K][RT];
 #pragma unroll
   for (int s = 0; s < K; ++s) {
-    const dbl2 fv = (s < nm && ok) ? ld2<false>(win.F + (int64_t)s * ld + i0) : dbl2{0.0, 0.0};
-    fx[s] = fv.x;
-    fy[s] = fv.y;
+    Rows<RT> fv{};
+    if (s < nm) ld_rows<RT, false>(fv, win.F + (int64_t)s * ld + i0, okp);
+#pragma unroll
+    for (int u = 0; u < RT; ++u) f[s][u] = fv.v[u];
   }
+  const double* __restrict__ P = win.P;
+  const uint32_t ep = *win.epoch & TAG_EPOCH;
+  // alternate the sweep direction per window: the columns a flush starts with
+  // are the ones the previous flush wrote last (still in the Infinity Cache)
+  ColCursor cur{win.tag, g, G, (N - g + G - 1) / G, 0, ep, 0u, 0u, 0ull,
+                ALT && (ep & 1u) != 0};
+  cur.start(lane);
   int64_t touched = 0;
-  const int64_t ncol_g = (N - g + G - 1) / G;  // columns g + G*k of this group
-  for (int64_t kb = 0; kb < ncol_g; kb += BLK) {
-    // 1. compact this batch's tagged columns into the LDS list (entry = k | flags)
-    const int64_t k = kb + threadIdx.x;
-    const uint32_t tg = (k < ncol_g) ? win.tag[g + k * G] : 0u;
-    const bool hit = k < ncol_g && (tg & TAG_EPOCH) == epoch;
-    const uint64_t msk = __ballot(hit);
-    __syncthreads();  // the previous batch is consumed
-    if (lane == 0) wcnt[wid] = __popcll(msk);
-    __syncthreads();
-    int off = 0, cnt = 0;
+  int64_t jr[D];
+  uint32_t fr[D];
+  bool hv[D];
+  Rows<RT> t[D];
 #pragma unroll
-    for (int w = 0; w < NWAVE; ++w) {
-      off += (w < wid) ? wcnt[w] : 0;
-      cnt += wcnt[w];
-    }
-    if (hit)
-      list[off + __popcll(msk & ((1ull << lane) - 1ull))] =
-          (uint32_t)threadIdx.x | (tg & (TAG_SPECIAL | TAG_ZERO));
-    __syncthreads();
-    // 2. stage p_s[j] of the listed columns: pls[e*K + s]
-    for (int x = threadIdx.x; x < cnt * K; x += BLK) {
-      const int e = x / K, s = x % K;
-      const int64_t j = g + (kb + (int64_t)(list[e] & 0xffffu)) * G;
-      pls[x] = win.P[j * KW + s];
-    }
-    __syncthreads();
-    touched += cnt;
-    // 3. stream the listed columns, two at a time, the next two prefetched
-    dbl2 t[CB];
+  for (int b = 0; b < D; ++b) {
+    hv[b] = cur.next(jr[b], fr[b], lane);  // stays false once the group is exhausted
+    if (hv[b]) ld_rows<RT, false>(t[b], A + jr[b] * ld + i0, okp);
+  }
+  // p_s[j] in SGPRs: K <= 8 keeps the next column's p in flight as well;
+  // larger windows load p in chunks of 16 slots at the column (SGPR budget)
+  constexpr bool PN = K <= 8;
+  constexpr int PCH = K < 16 ? K : 16;
+  double pc[PCH];
+  if (PN && hv[0]) {
 #pragma unroll
-    for (int b = 0; b < CB; ++b)
-      if (b < cnt && ok) t[b] = ld2<false>(A + (g + (kb + (int64_t)(list[b] & 0xffffu)) * G) * ld + i0);
-    for (int e0 = 0; e0 < cnt; e0 += CB) {
-      dbl2 tn[CB];
+    for (int s = 0; s < PCH; ++s) pc[s] = P[jr[0] * KW + s];
+  }
+  // slots are refilled round-robin, so once one finds the group exhausted every
+  // later one does too: an iteration with hv[0] false has nothing left
+  while (hv[0]) {
 #pragma unroll
-      for (int b = 0; b < CB; ++b) {
-        const int e = e0 + CB + b;
-        if (e < cnt && ok)
-          tn[b] = ld2<false>(A + (g + (kb + (int64_t)(list[e] & 0xffffu)) * G) * ld + i0);
+    for (int b = 0; b < D; ++b) {
+      if (!hv[b]) continue;
+      const int bn = (b + 1) % D;
+      double pn[PCH];  // PN: the next column's p, in flight during this update
+      if (PN && hv[bn]) {
+#pragma unroll
+        for (int s = 0; s < PCH; ++s) pn[s] = P[jr[bn] * KW + s];
       }
+      const int64_t j = jr[b];
+      Rows<RT> x = t[b];
+      const bool fast = full && !fr[b];
 #pragma unroll
-      for (int b = 0; b < CB; ++b) {
-        const int e = e0 + b;
-        if (e < cnt) {
-          const uint32_t le = list[e];
-          const int64_t j = g + (kb + (int64_t)(le & 0xffffu)) * G;
-          const double* __restrict__ pe = pls + e * K;
-          dbl2 x = t[b];
-          if (full && !(le & (TAG_SPECIAL | TAG_ZERO))) {
+      for (int s0 = 0; s0 < K; s0 += PCH) {
+        if (!PN) {
 #pragma unroll
-            for (int s = 0; s < K; ++s) {
-              const double p = pe[s];
-              x.x = msub(x.x, fx[s], p);
-              x.y = msub(x.y, fy[s], p);
-            }
-          } else {
-            for (int s = 0; s < nm; ++s) {
-              const int64_t rl = win.r[s] - row0;
-              const int64_t cs = win.c[s];
-              const double* __restrict__ Fs = win.F + (int64_t)s * ld;
-              const double p = pe[s];
-              x.x = apply_pivot(x.x, i0, j, rl, cs, ok ? Fs[i0] : 0.0, p, skip);
-              x.y = apply_pivot(x.y, i0 + 1, j, rl, cs, ok ? Fs[i0 + 1] : 0.0, p, skip);
+          for (int s = 0; s < PCH; ++s) pc[s] = P[j * KW + s0 + s];
+        }
+        if (fast) {
+#pragma unroll
+          for (int s = 0; s < PCH; ++s)
+#pragma unroll
+            for (int u = 0; u < RT; ++u) x.v[u] = msub(x.v[u], f[s0 + s][u], pc[s]);
+        } else {
+#pragma unroll
+          for (int s = 0; s < PCH; ++s) {
+            if (s0 + s < nm) {
+              const int64_t rl = win.r[s0 + s] - row0;
+              const int64_t cs = win.c[s0 + s];
+#pragma unroll
+              for (int u = 0; u < RT; ++u)
+                x.v[u] = apply_pivot(x.v[u], row_of<RT>(i0, u), j, rl, cs, f[s0 + s][u], pc[s],
+                                     skip);
             }
           }
-          if (ok) st2<NTS>(A + j * ld + i0, x);
         }
       }
+      st_rows<RT, NTS>(A + j * ld + i0, x, okp);
+      ++touched;
+      hv[b] = cur.next(jr[b], fr[b], lane);
+      if (hv[b]) ld_rows<RT, false>(t[b], A + jr[b] * ld + i0, okp);
+      if (PN) {
 #pragma unroll
-      for (int b = 0; b < CB; ++b) t[b] = tn[b];
+        for (int s = 0; s < PCH; ++s) pc[s] = pn[s];
+      }
     }
   }
   if (chunk == 0 && threadIdx.x == 0) {
@@ -386,6 +544,8 @@ __global__ __launch_bounds__(BLK) void flush_kernel(double* __restrict__ A, int6
               (unsigned long long)touched);
     if (g == 0) st->iters += nm;
   }
+  SPX_PROBE(K, 2, 1, true);
+  SPX_PROBE_BLOCK(1);
 }
 
 // ---------------------------------------------------------------------------
@@ -397,29 +557,45 @@ __global__ __launch_bounds__(BLK) void flush_kernel(double* __restrict__ A, int6
 // ---------------------------------------------------------------------------
 template <int K>
 __global__ __launch_bounds__(BLK) void row_fix_kernel(double* __restrict__ A, int64_t ld,
-                                                      int64_t row0, int64_t N, Window win) {
-  int nm = 0;
-  for (int s = 0; s < K; ++s) nm += win.made[s];
-  if (nm != K) return;
+                                                      int64_t m_local, int64_t row0, int64_t N,
+                                                      Window win) {
+  __shared__ double fr[K][K];  // fr[L][s] = f_s[r_L]
+  __shared__ int64_t rows[K];
+  __shared__ int lastL[K];
+  // all loads are independent: issue them together
   const int64_t j = (int64_t)blockIdx.x * BLK + threadIdx.x;
-  if (j >= N) return;
+  const bool live = j < N;
+  const uint32_t tg = live ? win.tag[j] : 0u;
   const uint32_t epoch = *win.epoch & TAG_EPOCH;
-  const uint32_t tg = win.tag[j];
-  if ((tg & TAG_EPOCH) != epoch || (tg & (TAG_SPECIAL | TAG_ZERO))) return;
+  int madeK = 0;
+  for (int s = 0; s < K; ++s) madeK += win.made[s];
   double p[K];
 #pragma unroll
-  for (int s = 0; s < K; ++s) p[s] = win.P[j * KW + s];
-  for (int L = 0; L < K; ++L) {
-    const int64_t r = win.r[L];
+  for (int s = 0; s < K; ++s) p[s] = win.P[(live ? j : 0) * KW + s];
+  // (loaded before the made-count check: a slot not made in this window holds a
+  // stale row, so the index is clamped; such values are never used)
+  for (int x = threadIdx.x; x < K * K; x += BLK) {
+    const int L = x / K, s = x % K;
+    const int64_t rl = min(max(win.r[L] - row0, (int64_t)0), m_local - 1);
+    fr[L][s] = win.F[(int64_t)s * ld + rl];
+  }
+  if (threadIdx.x < K) {
+    const int64_t r = win.r[threadIdx.x];
     bool last = true;
-    for (int s = L + 1; s < K; ++s) last &= win.r[s] != r;
-    if (!last) continue;
-    const int64_t rl = r - row0;
+    for (int s = threadIdx.x + 1; s < K; ++s) last &= win.r[s] != r;
+    rows[threadIdx.x] = r - row0;
+    lastL[threadIdx.x] = last;
+  }
+  __syncthreads();
+  if (madeK != K || !live || (tg & TAG_EPOCH) != epoch || (tg & (TAG_SPECIAL | TAG_ZERO)))
+    return;
+#pragma unroll
+  for (int L = 0; L < K; ++L) {
+    if (!lastL[L]) continue;
     double x = p[L];
 #pragma unroll
-    for (int s = 0; s < K; ++s)
-      if (s > L) x = msub(x, win.F[(int64_t)s * ld + rl], p[s]);
-    A[j * ld + rl] = x;
+    for (int s = L + 1; s < K; ++s) x = msub(x, fr[L][s], p[s]);
+    A[j * ld + rows[L]] = x;
   }
 }
 

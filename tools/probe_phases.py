@@ -1,0 +1,103 @@
+"""Phase timing of one window's kernels (diagnostic; not part of the product).
+
+Builds lib/libspx_probe.so with -DSPX_PHASE_TIMING (block 0 / thread 0 of every
+window kernel stamps s_memrealtime, 100 MHz, at its phase boundaries), runs
+windows on the config-3 tableau through it and prints, for the last window,
+each kernel's phase times relative to the window start (us).
+
+usage: python tools/probe_phases.py [--window 16] [--m 8192 --n 8192] [--build-only]
+"""
+import argparse
+import ctypes
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(ROOT, "simplex-solver_amd")
+LIB = os.path.join(PKG, "simplex_amd", "lib", "libspx_probe.so")
+
+
+def build():
+    cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC",
+           "-shared", "-ffp-contract=off", "-DSPX_PHASE_TIMING", "-o", LIB,
+           os.path.join(PKG, "csrc", "spx_capi.hip"), "-lrccl"]
+    subprocess.run(cmd, check=True)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--window", type=int, default=16)
+    ap.add_argument("--m", type=int, default=8192)
+    ap.add_argument("--n", type=int, default=8192)
+    ap.add_argument("--build-only", action="store_true")
+    ap.add_argument("--fv", type=int, default=0)
+    a = ap.parse_args()
+    if a.build_only or not os.path.exists(LIB):
+        build()
+        if a.build_only:
+            return
+    os.environ["SPX_LIB"] = LIB
+    sys.path.insert(0, PKG)
+    from simplex_amd import synth
+    from simplex_amd.engine import DeviceTableau
+    K = a.window
+    Tf, obj, basis = synth.tableau_rows("dense", a.m, a.n, 20251205, order="F")
+    e = DeviceTableau(0)
+    e.set_window(K)
+    e.load_rows(Tf, obj, basis, a.m, 0)
+    v = e.elim_variant()
+    e.set_elim_variant(0, 0, -1, (v["interleave"] | (0 if v["pipeline"] else 2)) | (a.fv << 8))
+    del Tf
+    e.run_pivots(4 * K)
+    e.sync()
+    e.run_pivots(K)  # one window: its stamps overwrite the buffer
+    e.sync()
+    lib = ctypes.CDLL(LIB)
+    NB = 1024 + 2 * 8192
+    buf = (ctypes.c_ulonglong * NB)()
+    assert lib.spx_probe_read(buf, NB) == 0
+    t = lambda slot, kind, ph: buf[((slot * 4 + kind) * 4 + ph) & 1023]
+    t0 = t(0, 0, 0)
+    us = lambda x: (x - t0) / 100.0
+    names = {0: "lazy_ratio", 1: "lazy_norm"}
+    print(f"window K={K}, m={a.m}, n={a.n}: us from lazy_ratio(0) entry (block 0, thread 0)")
+    prev_end = None
+    for q in range(K):
+        for kind in (0, 1):
+            ph = [us(t(q, kind, p)) for p in range(4)]
+            gap = ph[0] - prev_end if prev_end is not None else 0.0
+            print(f"q={q:2d} {names[kind]:10s} entry {ph[0]:8.2f} (+{gap:5.2f} after prev end)"
+                  f"  phase1 +{ph[1]-ph[0]:5.2f}  phase2 +{ph[2]-ph[1]:5.2f}"
+                  f"  end +{ph[3]-ph[2]:5.2f}  total {ph[3]-ph[0]:5.2f}")
+            prev_end = ph[3]
+    f0, f1 = us(t(K, 2, 0)), us(t(K, 2, 1))
+    print(f"flush entry {f0:8.2f} (+{f0 - prev_end:5.2f})  block-0 duration {f1 - f0:7.2f}")
+    rch, G = ctypes.c_int(), ctypes.c_int()
+    lib.spx_probe_flush_grid.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int),
+                                         ctypes.POINTER(ctypes.c_int)]
+    lib.spx_probe_flush_grid(e._ctx, ctypes.byref(rch), ctypes.byref(G))
+    nblk = min(rch.value * G.value, 8192)
+    import numpy as np
+    st = np.array([buf[1024 + 2 * b] for b in range(nblk)], dtype=np.float64)
+    en = np.array([buf[1024 + 2 * b + 1] for b in range(nblk)], dtype=np.float64)
+    st, en = (st - t0) / 100.0 - f0, (en - t0) / 100.0 - f0
+    dur = en - st
+    print(f"flush grid {rch.value} row chunks x {G.value} groups = {nblk} blocks")
+    q = lambda a: " ".join(f"{x:7.1f}" for x in np.percentile(a, [0, 10, 50, 90, 100]))
+    print(f"  block start  pct 0/10/50/90/100: {q(st)}")
+    print(f"  block end    pct 0/10/50/90/100: {q(en)}")
+    print(f"  block dur    pct 0/10/50/90/100: {q(dur)}")
+    g = np.arange(nblk) // rch.value
+    gd = np.array([dur[g == k].mean() for k in range(G.value)])
+    print(f"  per-group mean dur min/median/max: {gd.min():.1f} {np.median(gd):.1f} {gd.max():.1f}")
+    ch = np.arange(nblk) % rch.value
+    cd = np.array([dur[ch == k].mean() for k in range(rch.value)])
+    print("  per-chunk mean dur:", " ".join(f"{x:.0f}" for x in cd))
+    xcd = np.arange(nblk) % 8
+    print("  per-XCD mean dur:", " ".join(f"{dur[xcd == k].mean():.0f}" for k in range(8)))
+    e.close()
+
+
+if __name__ == "__main__":
+    main()
