@@ -48,7 +48,7 @@ def parse():
     ap.add_argument("--R", type=int, default=0, help="elim rows per thread (0: auto)")
     ap.add_argument("--wgs", type=int, default=0, help="elim grid target (0: auto)")
     ap.add_argument("--fv", type=int, default=-1,
-                    help="windowed flush variant 0-4 (rows/thread x ring depth; -1 default)")
+                    help="windowed flush variant 0-7 (0: LDS-DMA ring of 12, the default; see spx_capi.hip)")
     ap.add_argument("--graph", type=int, default=1,
                     help="1: the timed region replays one hipGraph with an event pair "
                          "captured around every elimination; 0: direct launches + events")

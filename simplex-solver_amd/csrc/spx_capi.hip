@@ -200,6 +200,8 @@ int free_buffers(spx_ctx* ctx) {
   dfree(ctx->win.made);
   dfree(ctx->win.tag);
   dfree(ctx->win.epoch);
+  dfree(ctx->win.nlist);
+  dfree(ctx->win.rec);
   ctx->loaded = false;
   return SPX_OK;
 }
@@ -368,6 +370,7 @@ int enqueue_window_t(spx_ctx* ctx, int npiv, bool time_flush) {
                        ctx->prm, ctx->st);
     hipLaunchKernelGGL(lazy_norm_kernel<KMAX>, dim3(ctx->nbn), dim3(BLK), 0, ctx->stream,
                        ctx->A, ctx->ld, ctx->m_local, ctx->row0, ctx->N, ctx->obj, ctx->win, q,
+                       npiv - 1,
                        ctx->ratio_part, NWAVE * nbw, ctx->enter_part, ctx->basis, ctx->hist,
                        ctx->prm, ctx->st);
   }
@@ -394,15 +397,19 @@ int enqueue_window_t(spx_ctx* ctx, int npiv, bool time_flush) {
                        ctx->st);
   };
   const bool nts = (ctx->elim_nt & 2) != 0;
-  // variants (rows per thread RT x register-ring depth D; A: sweep direction
-  // alternating per window): 0 2x4A (default), 1 2x4, 2 4x4, 3 4x4A, 4 2x8
-  // (profiles/r01/tune_flush_*.log)
+  // variants: 0 (default) LDS-DMA ring of 12 columns per wave over the
+  // compacted records; 6 / 7 the same with rings of 9 / 16; register rings
+  // (rows per lane x depth, A = sweep direction alternating per window):
+  // 1 2x4, 2 4x4, 3 4x4A, 4 2x8, 5 2x4A (profiles/r01/tune_flush_*.log)
   switch (ctx->flush_var) {
     case 1: nts ? go(flush_kernel<KMAX, 2, 4, true>, 2) : go(flush_kernel<KMAX, 2, 4, false>, 2); break;
     case 2: nts ? go(flush_kernel<KMAX, 4, 4, true>, 4) : go(flush_kernel<KMAX, 4, 4, false>, 4); break;
     case 3: nts ? go(flush_kernel<KMAX, 4, 4, true, true>, 4) : go(flush_kernel<KMAX, 4, 4, false, true>, 4); break;
     case 4: nts ? go(flush_kernel<KMAX, 2, 8, true>, 2) : go(flush_kernel<KMAX, 2, 8, false>, 2); break;
-    default: nts ? go(flush_kernel<KMAX, 2, 4, true, true>, 2) : go(flush_kernel<KMAX, 2, 4, false, true>, 2);
+    case 5: nts ? go(flush_kernel<KMAX, 2, 4, true, true>, 2) : go(flush_kernel<KMAX, 2, 4, false, true>, 2); break;
+    case 6: nts ? go(flush_lds_kernel<KMAX, 9, true>, 2) : go(flush_lds_kernel<KMAX, 9, false>, 2); break;
+    case 7: nts ? go(flush_lds_kernel<KMAX, 16, true>, 2) : go(flush_lds_kernel<KMAX, 16, false>, 2); break;
+    default: nts ? go(flush_lds_kernel<KMAX, 12, true>, 2) : go(flush_lds_kernel<KMAX, 12, false>, 2);
   }
   if (e) {
     const int rc = record_event(ctx, e->second);
@@ -589,6 +596,10 @@ int alloc_common(spx_ctx* ctx, int64_t m_local, int64_t N, int64_t m_global, int
     HIPC(hipMalloc(&ctx->win.made, sizeof(int32_t) * KW));
     HIPC(hipMalloc(&ctx->win.tag, sizeof(uint32_t) * N));
     HIPC(hipMalloc(&ctx->win.epoch, sizeof(uint32_t)));
+    HIPC(hipMalloc(&ctx->win.nlist, sizeof(int32_t)));
+    HIPC(hipMalloc(&ctx->win.rec, sizeof(double) * RECW * N));
+    HIPC(hipMemsetAsync(ctx->win.nlist, 0, sizeof(int32_t), ctx->stream));
+    HIPC(hipMemsetAsync(ctx->win.rec, 0, sizeof(double) * RECW * N, ctx->stream));
     HIPC(hipMemsetAsync(ctx->win.F, 0, sizeof(double) * KW * ctx->ld, ctx->stream));
     HIPC(hipMemsetAsync(ctx->win.P, 0, sizeof(double) * KW * N, ctx->stream));
     HIPC(hipMemsetAsync(ctx->win.made, 0, sizeof(int32_t) * KW, ctx->stream));

@@ -73,7 +73,11 @@ struct Window {
   int32_t* made;     // KW            : 1 if pivot s of this window was made
   uint32_t* tag;     // N             : epoch (+ flags) of the last window touching column j
   uint32_t* epoch;   // 1             : current window number (bumped by lazy_ratio slot 0)
+  int32_t* nlist;    // 1             : records in `rec` (reset by lazy_ratio slot 0)
+  double* rec;       // N x RECW      : the window's touched columns, compacted by the
+                     //                 last lazy_norm: [j | path flags, pad, p_0 .. p_{K-1}]
 };
+constexpr int RECW = KW + 2;  // doubles per record (272 B)
 
 // Apply pending pivot s to value v at (local row il, column j).
 __device__ __forceinline__ double apply_pivot(double v, int64_t il, int64_t j, int64_t rl_s,
@@ -145,6 +149,12 @@ __global__ __launch_bounds__(BLK) void lazy_ratio_kernel(
     rls[s] = win.r[s] - row0;
     cs[s] = win.c[s];
   }
+  if (q == 0 && blockIdx.x == 0 && threadIdx.x == 0) {
+    // a new window, also when it ends before its first pivot (lazy_norm's
+    // compaction and the flush read these later; nothing in this launch does)
+    *win.epoch += 1;
+    *win.nlist = 0;
+  }
   if (status != ST_RUNNING) return;
   int64_t c;
   if (forced_c >= 0) {
@@ -165,7 +175,6 @@ __global__ __launch_bounds__(BLK) void lazy_ratio_kernel(
     st->c_next = c;
     st->zc_next = obj[c];
     st->n_ratio_part = gridDim.x * NWAVE;
-    if (q == 0) *win.epoch += 1;  // a new window (lazy_norm / flush read it later)
   }
   const int64_t rhs = N - 1;
   double fv = live ? A[c * ld + i] : 0.0;
@@ -216,7 +225,7 @@ __global__ __launch_bounds__(BLK) void lazy_ratio_kernel(
 template <int KMAX>
 __global__ __launch_bounds__(BLK) void lazy_norm_kernel(
     const double* __restrict__ A, int64_t ld, int64_t m_local, int64_t row0, int64_t N,
-    double* __restrict__ obj, Window win, int q, const Key* __restrict__ ratio_part,
+    double* __restrict__ obj, Window win, int q, int last, const Key* __restrict__ ratio_part,
     int n_ratio, Key* __restrict__ enter_part, int64_t* __restrict__ basis,
     int64_t* __restrict__ hist, const Params* __restrict__ prm, State* st) {
   const bool block0 = blockIdx.x == 0 && threadIdx.x == 0;
@@ -252,87 +261,110 @@ __global__ __launch_bounds__(BLK) void lazy_norm_kernel(
     rls[s] = win.r[s] - row0;
     cs[s] = win.c[s];
   }
-  if (status != ST_RUNNING) {
-    if (block0) win.made[q] = 0;
-    return;
-  }
-  if (c < 0 || (forced_r < 0 && it >= iter_limit)) {
-    if (block0) {
-      st->status = (c < 0) ? ST_OPTIMAL : ST_LIMIT;
-      win.made[q] = 0;
-    }
-    return;
+  // stop: no pivot in this slot (grid-uniform); the window's last slot still
+  // compacts the columns the earlier slots touched
+  bool stop = status != ST_RUNNING;
+  if (!stop && (c < 0 || (forced_r < 0 && it >= iter_limit))) {
+    if (block0) st->status = (c < 0) ? ST_OPTIMAL : ST_LIMIT;
+    stop = true;
   }
   int64_t r = forced_r;
-  if (r < 0) {
+  if (!stop && r < 0) {
     wave_min(rk);
     if (rk.row < 0) {
-      if (block0) {
-        st->status = ST_UNBOUNDED;
-        win.made[q] = 0;
-      }
-      return;
+      if (block0) st->status = ST_UNBOUNDED;
+      stop = true;
     }
     r = rk.row;
   }
-  SPX_PROBE(q, 1, 1, r >= 0);
-  const int64_t rl = r - row0;
-  const double piv = win.F[(int64_t)q * ld + rl];
-  double v = live ? A[j * ld + rl] : 0.0;
+  if (stop && block0) win.made[q] = 0;
+  uint32_t tg = old;  // this column's tag after this slot
+  double p = 0.0;
+  if (!stop) {
+    SPX_PROBE(q, 1, 1, r >= 0);
+    const int64_t rl = r - row0;
+    const double piv = win.F[(int64_t)q * ld + rl];
+    double v = live ? A[j * ld + rl] : 0.0;
 #pragma unroll
-  for (int s0 = 0; s0 < KMAX; s0 += 8) {
-    if (s0 < q) {
-      double fr[8];
+    for (int s0 = 0; s0 < KMAX; s0 += 8) {
+      if (s0 < q) {
+        double fr[8];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) fr[u] = win.F[(int64_t)(s0 + u) * ld + rl];
+        for (int u = 0; u < 8; ++u) fr[u] = win.F[(int64_t)(s0 + u) * ld + rl];
 #pragma unroll
-      for (int u = 0; u < 8 && s0 + u < KMAX; ++u)
-        if (s0 + u < q) v = apply_pivot(v, rl, j, rls[s0 + u], cs[s0 + u], fr[u], ps[s0 + u], skip);
+        for (int u = 0; u < 8 && s0 + u < KMAX; ++u)
+          if (s0 + u < q) v = apply_pivot(v, rl, j, rls[s0 + u], cs[s0 + u], fr[u], ps[s0 + u], skip);
+      }
+    }
+    SPX_PROBE(q, 1, 2, v != 12345.678);
+    KeyR ek = keyr_none();
+    if (live) {
+      p = v / piv;
+      win.P[j * KW + q] = p;
+      const bool nz = (p != 0.0) || !skip;
+      if (j == c) {
+        o = 0.0;
+      } else if (nz) {
+        o = msub(o, zc, p);
+      }
+      obj[j] = o;
+      // tag: touched in this window; SPECIAL if it entered, ZERO if (skip on) one
+      // of its p_s[j] so far is zero
+      const bool tagged = (old & TAG_EPOCH) == epoch;
+      bool zb = false;
+#pragma unroll
+      for (int s = 0; s < KMAX; ++s)
+        if (s < q) zb |= skip && ps[s] == 0.0;
+      if (nz) {
+        tg = epoch | ((j == c || (tagged && (old & TAG_SPECIAL))) ? TAG_SPECIAL : 0u) |
+             (zb ? TAG_ZERO : 0u);
+      } else if (tagged) {
+        tg = old | TAG_ZERO;
+      }
+      if (tg != old) win.tag[j] = tg;
+      if (j < n_enter && o < -eps_opt) kmin(ek, (rule == RULE_BLAND) ? 0.0 : o, j, j);
+    }
+    wave_min(ek);  // one entering partial per wave
+    if ((threadIdx.x & 63) == 0) store_key(enter_part + blockIdx.x * NWAVE + (threadIdx.x >> 6), ek);
+    if (block0) {
+      st->r = r;
+      st->c = c;
+      st->zc = zc;
+      st->piv = piv;
+      win.r[q] = r;
+      win.c[q] = c;
+      win.made[q] = 1;
+      basis[r] = c;
+      if (it < st->hist_cap) {
+        hist[2 * it] = r;
+        hist[2 * it + 1] = c;
+      }
     }
   }
-  SPX_PROBE(q, 1, 2, v != 12345.678);
-  KeyR ek = keyr_none();
-  if (live) {
-    const double p = v / piv;
-    win.P[j * KW + q] = p;
-    const bool nz = (p != 0.0) || !skip;
-    if (j == c) {
-      o = 0.0;
-    } else if (nz) {
-      o = msub(o, zc, p);
+  if (q == last) {
+    // compact this window's touched columns into records for the flush: wave
+    // ballot + LDS prefix over the 4 waves + one atomic per block
+    const bool mine = live && (tg & TAG_EPOCH) == epoch;
+    __shared__ int wcnt[NWAVE];
+    __shared__ int base;
+    const uint64_t bal = __ballot(mine);
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    if (lane == 0) wcnt[w] = __popcll(bal);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      int tot = 0;
+      for (int x = 0; x < NWAVE; ++x) tot += wcnt[x];
+      base = tot ? atomicAdd(win.nlist, tot) : 0;
     }
-    obj[j] = o;
-    // tag: touched in this window; SPECIAL if it entered, ZERO if (skip on) one
-    // of its p_s[j] so far is zero
-    const bool tagged = (old & TAG_EPOCH) == epoch;
-    bool zb = false;
+    __syncthreads();
+    int pos = base + __popcll(bal & ((1ull << lane) - 1ull));
+    for (int x = 0; x < w; ++x) pos += wcnt[x];
+    if (mine && pos < N) {  // (pos < N always: one epoch tags each column once)
+      double* rc_ = win.rec + (int64_t)pos * RECW;
+      reinterpret_cast<int64_t*>(rc_)[0] = j | ((int64_t)(tg >> 30) << 32);
 #pragma unroll
-    for (int s = 0; s < KMAX; ++s)
-      if (s < q) zb |= skip && ps[s] == 0.0;
-    uint32_t nt = old;
-    if (nz) {
-      nt = epoch | ((j == c || (tagged && (old & TAG_SPECIAL))) ? TAG_SPECIAL : 0u) |
-           (zb ? TAG_ZERO : 0u);
-    } else if (tagged) {
-      nt = old | TAG_ZERO;
-    }
-    if (nt != old) win.tag[j] = nt;
-    if (j < n_enter && o < -eps_opt) kmin(ek, (rule == RULE_BLAND) ? 0.0 : o, j, j);
-  }
-  wave_min(ek);  // one entering partial per wave
-  if ((threadIdx.x & 63) == 0) store_key(enter_part + blockIdx.x * NWAVE + (threadIdx.x >> 6), ek);
-  if (block0) {
-    st->r = r;
-    st->c = c;
-    st->zc = zc;
-    st->piv = piv;
-    win.r[q] = r;
-    win.c[q] = c;
-    win.made[q] = 1;
-    basis[r] = c;
-    if (it < st->hist_cap) {
-      hist[2 * it] = r;
-      hist[2 * it + 1] = c;
+      for (int s = 0; s < KMAX; ++s)
+        if (s <= q) rc_[2 + s] = (s < q) ? ps[s] : p;
     }
   }
   SPX_PROBE(q, 1, 3, true);
@@ -544,6 +576,152 @@ __global__ __launch_bounds__(BLK) void flush_kernel(double* __restrict__ A, int6
               (unsigned long long)touched);
     if (g == 0) st->iters += nm;
   }
+  SPX_PROBE(K, 2, 1, true);
+  SPX_PROBE_BLOCK(1);
+}
+
+// ---------------------------------------------------------------------------
+// flush_lds_kernel<K, D, NTS>: the same update as flush_kernel, over the
+// window's compacted records (lazy_norm, last slot), with the column loads
+// in flight in LDS instead of VGPRs.  Each wave owns a ring of D 1-KiB LDS
+// slots and walks its group's records g, g+G, ... on its own (no block
+// barrier): per column one global_load_lds_dwordx4 (128 rows x 8 B) issued D
+// columns ahead, one ds_read_b128, the msub chain with p_s[j] in SGPRs (the
+// record's p values, loaded one column ahead from an address that depends on
+// nothing), one global store.  Per-wave VMEM order is fixed -- one LDS-DMA
+// and one store per column (a dummy DMA past the end) -- so a constant
+// `s_waitcnt vmcnt(2*(D-1))` retires exactly the slot about to be read.
+// Bytes in flight per CU: waves x D KiB (16 x 8 = 128 KiB at K = 16) without
+// spending VGPRs on the ring, which the f_s registers (2K per lane) need.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void glds16(const void* gsrc, uint32_t lds_dst) {
+  // M0 = wave-uniform LDS byte base; each lane's 16 B land at base + lane*16
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %2\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, off\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(gsrc), "s"(lds_dst)
+      : "memory");
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+template <int K, int D, bool NTS>
+__global__ __launch_bounds__(BLK) void flush_lds_kernel(double* __restrict__ A, int64_t ld,
+                                                        int64_t m_local, int64_t row0,
+                                                        int64_t N, Window win, int npiv,
+                                                        int rch, int G,
+                                                        const Params* __restrict__ prm,
+                                                        State* st) {
+  static_assert(D >= 2 && D <= 16, "ring depth");
+  __shared__ dbl2 ring[NWAVE * D * 64];
+  SPX_PROBE(K, 2, 0, true);
+  SPX_PROBE_BLOCK(0);
+  int nm = 0;  // pivots made in this window: a prefix of its npiv slots
+  for (int s = 0; s < npiv; ++s) nm += win.made[s];
+  const int L = *win.nlist;
+  if (nm == 0) return;
+  const bool full = nm == K;
+  const bool skip = prm->skip_zero != 0;
+  const int chunk = blockIdx.x % rch;
+  const int g = blockIdx.x / rch;
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform, in an SGPR
+  if (chunk == 0 && g == 0 && threadIdx.x == 0) {
+    atomicAdd(reinterpret_cast<unsigned long long*>(&st->touched_total), (unsigned long long)L);
+    st->iters += nm;
+  }
+  const int64_t wrow = (int64_t)chunk * 2 * BLK + (int64_t)w * 128;  // this wave's first row
+  if (wrow >= m_local || g >= L) return;  // wave-uniform: nothing to do
+  const int cnt = (L - g + G - 1) / G;    // this wave's records: g, g+G, ...
+  const int64_t i0 = wrow + 2 * lane;
+  const bool ok = i0 < m_local;            // the pair (i0, i0+1) holds local rows
+  const int64_t i0c = ok ? i0 : wrow;      // in-column address for idle lanes
+  double f[K][2];
+#pragma unroll
+  for (int s = 0; s < K; ++s) {
+    dbl2 fv = dbl2{0.0, 0.0};
+    if (s < nm && ok) fv = ld2<false>(win.F + (int64_t)s * ld + i0);
+    f[s][0] = fv.x;
+    f[s][1] = fv.y;
+  }
+  // records, r_s and c_s through the constant address space: uniform loads
+  // from it are always scalar (SMEM, lgkmcnt), so no VMEM op joins the
+  // per-column count below
+  typedef const __attribute__((address_space(4))) double cdbl;
+  typedef const __attribute__((address_space(4))) int64_t ci64;
+  cdbl* rec = (cdbl*)win.rec;
+  ci64* hdr = (ci64*)win.rec;
+  ci64* wr = (ci64*)win.r;
+  ci64* wc = (ci64*)win.c;
+  auto rec_of = [&](int k) -> int64_t { return (int64_t)(g + (int64_t)k * G) * RECW; };
+  const uint32_t lds0 =
+      (uint32_t)(uintptr_t)((__attribute__((address_space(3))) dbl2*)&ring[0]) +
+      (uint32_t)(w * D * 64) * (uint32_t)sizeof(dbl2);
+  // f must be in registers before the first DMA: the compiler does not see
+  // the DMAs, and a wait it placed inside the loop for f would drain them
+#pragma unroll
+  for (int s = 0; s < K; ++s) asm volatile("" ::"v"(f[s][0]), "v"(f[s][1]));
+  wait_vmcnt<0>();
+  // prologue: columns 0..D-1 (a dummy re-read of the last real column past cnt)
+  const double* last_src = A + (hdr[rec_of(0)] & 0xffffffffll) * ld + i0c;
+#pragma unroll
+  for (int d = 0; d < D; ++d) {
+    if (d < cnt) last_src = A + (hdr[rec_of(d)] & 0xffffffffll) * ld + i0c;
+    glds16(last_src, lds0 + (uint32_t)(d * 64 * sizeof(dbl2)));
+  }
+  int64_t hn = (D < cnt) ? hdr[rec_of(D)] : 0;  // header of column D (next DMA)
+  int64_t hc = hdr[rec_of(0)];                  // header of the column being updated
+  double pc[K];
+#pragma unroll
+  for (int s = 0; s < K; ++s) pc[s] = rec[rec_of(0) + 2 + s];
+  for (int k = 0; k < cnt; ++k) {
+    const int slot = k % D;
+    // retire column k's DMA: 2 VMEM ops per later column, fewer in the prologue
+    if (k >= D - 1) wait_vmcnt<2 * (D - 1)>();
+    else wait_vmcnt<D - 1>();
+    dbl2 x = ring[(w * D + slot) * 64 + lane];
+    const int64_t j = hc & 0xffffffffll;
+    const bool fast = full && (hc >> 32) == 0;
+    if (fast) {
+#pragma unroll
+      for (int s = 0; s < K; ++s) {
+        x.x = msub(x.x, f[s][0], pc[s]);
+        x.y = msub(x.y, f[s][1], pc[s]);
+      }
+    } else {
+#pragma unroll
+      for (int s = 0; s < K; ++s) {
+        if (s < nm) {
+          const int64_t rl = wr[s] - row0;
+          const int64_t cs = wc[s];
+          x.x = apply_pivot(x.x, i0, j, rl, cs, f[s][0], pc[s], skip);
+          x.y = apply_pivot(x.y, i0 + 1, j, rl, cs, f[s][1], pc[s], skip);
+        }
+      }
+    }
+    if (ok) st2<NTS>(A + j * ld + i0, x);
+    // DMA of column k + D into the slot just read (its ds_read has retired:
+    // x was consumed above); a dummy re-read keeps the VMEM count per column
+    if (k + D < cnt) last_src = A + (hn & 0xffffffffll) * ld + i0c;
+    glds16(last_src, lds0 + (uint32_t)(slot * 64 * sizeof(dbl2)));
+    // next column's header and p, and the header of the column after the
+    // next DMA: scalar loads issued after this column's ds_read has retired
+    // (LDS and SMEM share lgkmcnt), so they land during the next vmcnt wait
+    const int kn = k + 1 < cnt ? k + 1 : k;
+    hc = hdr[rec_of(kn)];
+#pragma unroll
+    for (int s = 0; s < K; ++s) pc[s] = rec[rec_of(kn) + 2 + s];
+    hn = (k + D + 1 < cnt) ? hdr[rec_of(k + D + 1)] : 0;
+  }
+  wait_vmcnt<0>();  // no DMA may land in LDS after the wave has exited
   SPX_PROBE(K, 2, 1, true);
   SPX_PROBE_BLOCK(1);
 }

@@ -57,6 +57,33 @@ def test_window_rule_pivots_bit_exact(eng_cls, K, shape, skip):
     assert out.tobytes() == out0.tobytes()
 
 
+def _set_flush_variant(e, fv):
+    v = e.elim_variant()
+    ilv = (v["interleave"] | (0 if v["pipeline"] else 2)) | (fv << 8)
+    e.set_elim_variant(0, 0, -1, ilv)
+
+
+@pytest.mark.parametrize("fv", range(8))
+@pytest.mark.parametrize("K", [2, 16, 32])
+@pytest.mark.parametrize("shape", [(17, 40), (700, 1500), (1537, 2600)])
+def test_window_flush_variants_bit_exact(eng_cls, fv, K, shape):
+    """Every flush kernel variant (register rings of 1/2/4 rows per lane, the
+    LDS-DMA ring over compacted records) gives the single-pivot bytes."""
+    T, basis = _random_tableau(*shape, seed=shape[0] + 3 * shape[1] + fv)
+    with eng_cls(0) as e:
+        e.set_window(K)
+        e.load(T, basis)
+        _set_flush_variant(e, fv)
+        res = e.solve(max_iters=3 * K + 5)
+        h, out = e.history().tolist(), e.tableau()
+    with eng_cls(0) as s:
+        s.load(T, basis)
+        res0 = s.solve(max_iters=3 * K + 5)
+        assert h == s.history().tolist()
+        assert res.status == res0.status and res.iters == res0.iters
+        assert out.tobytes() == s.tableau().tobytes()
+
+
 @pytest.mark.parametrize("K", [4, 16])
 def test_window_config2_full_solve(eng_cls, K):
     """BASELINE config 2 (1024 x 2048): every pivot, final tableau, objective."""
