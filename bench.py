@@ -56,8 +56,10 @@ def parse():
     ap.add_argument("--window", type=int, default=-1,
                     help="windowed elimination: K pivots per tableau pass (0 = off, "
                          "-1 = default: %d on one GPU, off when sharded)" % DEFAULT_WINDOW)
-    ap.add_argument("--time-every", type=int, default=8,
-                    help="HIP events around every k-th elimination of the timed region")
+    ap.add_argument("--time-every", type=int, default=0,
+                    help="HIP events around every k-th elimination (or window flush) of the "
+                         "timed region (0: 8 eliminations / 4 flushes; an event node costs "
+                         "~6 us of stream time)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0,
                     help="budget of the CPU-baseline sample (0 disables)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles",
@@ -183,7 +185,8 @@ def main():
     barrier()
     eng.sync()
     t0 = time.perf_counter()
-    eng.run_pivots(args.steps, time_elim=1 if K else args.time_every, **opts)
+    every = args.time_every if args.time_every > 0 else (4 if K else 8)
+    eng.run_pivots(args.steps, time_elim=every, **opts)
     eng.sync()
     t1 = time.perf_counter()
     barrier()
@@ -197,10 +200,10 @@ def main():
         raise SystemExit(f"pivot loop ended early: status {status}, iters {iters}")
     ms_tot, launches, touched = eng.elim_timing(reset=True)
     what = "flush (window pass)" if K else "elimination"
-    every = "every" if K else f"every {args.time_every}th"
-    window = (f"timed region: HIP event-record nodes around {every} {what} inside the "
-              f"replayed hipGraph, on the engine stream" if use_graph else
-              f"timed region: HIP events around {every} {what} launch")
+    every = f"every {every}th"
+    window = (f"timed region: HIP events on the engine stream around {every} {what}, "
+              f"launched directly" + ("; the other windows replay the per-window hipGraph"
+                                      if (use_graph and K) else ""))
     avg_ms = ms_tot / launches
     m_local = row1 - row0
     N = n + m + 1
@@ -251,7 +254,8 @@ def main():
                                     else f"config 4: config-3 tableau row-sharded x{world}"),
                        "m": m, "n": n, "tableau": [m + 1, N], "rule": args.rule,
                        "elimination": "dense sweep" if args.dense else "skip p[j]==0 columns",
-                       "timing": "hipGraph replay" if use_graph else "direct launches",
+                       "timing": ("per-window hipGraph replay" if (use_graph and K)
+                                  else "direct launches"),
                        "elim_variant": eng.elim_variant(),
                        "window": K,
                        "parallelism": f"row-shard x{world}" if world > 1 else "single GPU"},

@@ -89,26 +89,51 @@ __device__ __forceinline__ double apply_pivot(double v, int64_t il, int64_t j, i
 }
 
 // This lane's share (keys lane, lane+64, ...) of a per-wave argmin over n >= 1
-// keys: up to 8 keys per lane with every load issued before the first compare
-// (a plain strided loop waits one memory latency per key).  wave_min() after.
-__device__ __forceinline__ KeyR lane_keys(const Key* __restrict__ part, int n) {
+// keys, in two halves so the loads join the kernel's first batch of
+// independent loads: keys_issue() puts up to 8 keys per lane in flight
+// (clamped indices: no branch, no loop, nothing for the compiler to sink or
+// wait on early); keys_reduce() compares them (and walks any keys beyond 512,
+// which only a tableau of more than 32768 columns has).  wave_min() after.
+struct Keys8 {
+  dbl2 a[8], b[8];  // (v, t) and (row, pad) of keys lane + 64u
+};
+__device__ __forceinline__ void keys_issue(Keys8& K, const Key* __restrict__ part, int n) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    const dbl2* p = reinterpret_cast<const dbl2*>(part + min(lane + 64 * u, n - 1));
+    K.a[u] = p[0];
+    K.b[u] = p[1];
+  }
+}
+__device__ __forceinline__ KeyR keys_reduce(const Keys8& K, const Key* __restrict__ part, int n) {
   KeyR k = keyr_none();
   const int lane = threadIdx.x & 63;
-  for (int b = lane; b < n; b += 64 * 8) {
-    double v[8];
-    int64_t t[8], r[8];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int x = min(b + 64 * u, n - 1);
-      v[u] = part[x].v;
-      t[u] = part[x].t;
-      r[u] = part[x].row;
-    }
-#pragma unroll
-    for (int u = 0; u < 8; ++u)
-      if (b + 64 * u < n) kmin(k, v[u], t[u], r[u]);
-  }
+  for (int u = 0; u < 8; ++u)
+    if (lane + 64 * u < n)
+      kmin(k, K.a[u].x, __double_as_longlong(K.a[u].y), __double_as_longlong(K.b[u].x));
+  if (n > 512)
+    for (int x = lane + 512; x < n; x += 64) kmin(k, part[x].v, part[x].t, part[x].row);
   return k;
+}
+
+// Branchless application of pending pivot s to v at (row il, column j): the
+// slot's flags are wave-uniform, but a branch would let the compiler sink the
+// kernel's early loads below it (one more memory round trip per kernel).
+__device__ __forceinline__ double apply_sel(double v, bool il_is_r, bool j_is_c, bool active,
+                                            double f, double p, bool skip) {
+  const double upd = il_is_r ? p : msub(v, f, p);
+  double x = (skip && p == 0.0) ? v : upd;
+  x = j_is_c ? (il_is_r ? 1.0 : 0.0) : x;
+  return active ? x : v;
+}
+
+// v_readlane of an int64 held per lane (lane index wave-uniform).
+__device__ __forceinline__ int64_t rdlane64(int64_t v, int lane) {
+  const int lo = __builtin_amdgcn_readlane((int)(v & 0xffffffff), lane);
+  const int hi = __builtin_amdgcn_readlane((int)(v >> 32), lane);
+  return ((int64_t)hi << 32) | (uint32_t)lo;
 }
 
 // Fill n keys with "no candidate" (entering partials beyond norm<INIT>'s).
@@ -121,95 +146,99 @@ __global__ __launch_bounds__(BLK) void fill_none_kernel(Key* __restrict__ k, int
 // lazy_ratio_kernel<KMAX> (slot q < KMAX = number of pending pivots): entering
 // column of the coming pivot (or forced), its current values -> F[q], min-ratio
 // partials.  grid: ceil(m_local / BLK) blocks, one row per thread.
+// Two memory round trips on the critical path: (1) every load that does not
+// depend on the column -- entering partials, f_s of this row, the slots'
+// (r_s, c_s) lane-indexed, state -- in one batch; (2) after the argmin, the
+// stale column c and RHS and their p_s values.  Then stores only.
 // ---------------------------------------------------------------------------
 template <int KMAX>
 __global__ __launch_bounds__(BLK) void lazy_ratio_kernel(
-    const double* __restrict__ A, int64_t ld, int64_t m_local, int64_t row0, int64_t N,
-    const double* __restrict__ obj, Window win, int q, const Key* __restrict__ enter_part,
-    int n_enter_part, Key* __restrict__ ratio_part, const int64_t* __restrict__ basis,
-    const Params* __restrict__ prm, State* st) {
+    // the first loads' operands lead the list: they are preloaded into SGPRs
+    // (-amdgpu-kernarg-preload-count), so no kernarg fetch precedes them
+    const Key* __restrict__ enter_part, State* st, const Params* __restrict__ prm,
+    int n_enter_part, int q, const double* __restrict__ A, int64_t ld, int64_t m_local,
+    int64_t row0, int64_t N, const double* __restrict__ obj, Window win,
+    Key* __restrict__ ratio_part, const int64_t* __restrict__ basis) {
+  static_assert(KMAX <= 64, "slots are lane-indexed");
   SPX_PROBE(q, 0, 0, true);
-  // independent loads first: state, entering partials, this row's f_s
+  const bool block0 = blockIdx.x == 0 && threadIdx.x == 0;
+  const int lane = threadIdx.x & 63;
+  const int64_t i = (int64_t)blockIdx.x * BLK + threadIdx.x;
+  const bool live = i < m_local;
+  const int64_t ic = live ? i : 0;
+  // --- batch 1 ---
+  Keys8 kk;
+  keys_issue(kk, enter_part, n_enter_part);
+  // the keys first: loads retire in issue order, and the argmin must not wait
+  // for the f_s loads behind them
+  asm volatile("" ::: "memory");
+  double fs[KMAX];
+#pragma unroll
+  for (int s = 0; s < KMAX; ++s) fs[s] = win.F[(int64_t)s * ld + ic];
+  const int64_t slot_r = win.r[lane < KMAX ? lane : 0];
+  const int64_t slot_c = win.c[lane < KMAX ? lane : 0];
   const int32_t status = st->status;
   const int64_t forced_c = st->forced_c;
   const int32_t rule = prm->rule;
   const double eps_piv = prm->eps_piv;
   const bool skip = prm->skip_zero != 0;
-  KeyR e = lane_keys(enter_part, n_enter_part);  // per wave: no LDS round, no barrier
-  const int64_t i = (int64_t)blockIdx.x * BLK + threadIdx.x;
-  const bool live = i < m_local;
-  // slot data, loaded unconditionally (stale slots >= q are valid memory, unused)
-  // so no load waits behind a per-slot branch
-  double fs[KMAX];
-  int64_t rls[KMAX], cs[KMAX];
-  const int64_t ic = live ? i : 0;
-#pragma unroll
-  for (int s = 0; s < KMAX; ++s) {
-    fs[s] = win.F[(int64_t)s * ld + ic];
-    rls[s] = win.r[s] - row0;
-    cs[s] = win.c[s];
-  }
-  if (q == 0 && blockIdx.x == 0 && threadIdx.x == 0) {
+  if (q == 0 && block0) {
     // a new window, also when it ends before its first pivot (lazy_norm's
     // compaction and the flush read these later; nothing in this launch does)
     *win.epoch += 1;
     *win.nlist = 0;
   }
-  if (status != ST_RUNNING) return;
-  int64_t c;
-  if (forced_c >= 0) {
-    c = forced_c;
-  } else {
-    wave_min(e);
-    if (e.row < 0) {
-      if (blockIdx.x == 0 && threadIdx.x == 0) {
-        st->status = ST_OPTIMAL;
-        st->c_next = -1;
-      }
-      return;
-    }
-    c = e.row;
+  KeyR e = keys_reduce(kk, enter_part, n_enter_part);
+#ifdef SPX_PROBE_FINE
+  SPX_PROBE(q, 2, 0, e.v != 12345.678);
+#endif
+  wave_min_dpp(e);
+#ifdef SPX_PROBE_FINE
+  SPX_PROBE(q, 2, 1, e.v != 12345.678);
+#endif
+  const bool running = status == ST_RUNNING;
+  const int64_t c = (forced_c >= 0) ? forced_c : e.row;
+  const bool go = running && c >= 0;  // grid-uniform
+  if (block0 && running && c < 0) {
+    st->status = ST_OPTIMAL;
+    st->c_next = -1;
   }
-  SPX_PROBE(q, 0, 1, c >= 0);
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
-    st->c_next = c;
-    st->zc_next = obj[c];
-    st->n_ratio_part = gridDim.x * NWAVE;
-  }
+  SPX_PROBE(q, 0, 1, go);
+  // --- batch 2 (c clamped, so the loads are unconditional) ---
+  const int64_t cc = go ? c : 0;
   const int64_t rhs = N - 1;
-  double fv = live ? A[c * ld + i] : 0.0;
-  double bv = live ? A[rhs * ld + i] : 0.0;
-  const double* __restrict__ Pc = win.P + c * KW;
-  const double* __restrict__ Pb = win.P + rhs * KW;
-  // in chunks of 8 slots: the chunk's p values are loaded before its updates
+  double fv = A[cc * ld + ic];
+  double bv = A[rhs * ld + ic];
+  double pc[KMAX], pb[KMAX];
 #pragma unroll
-  for (int s0 = 0; s0 < KMAX; s0 += 8) {
-    if (s0 < q) {
-      double pc[8], pb[8];
+  for (int s = 0; s < KMAX; ++s) {
+    pc[s] = win.P[cc * KW + s];
+    pb[s] = win.P[rhs * KW + s];
+  }
+  const double zc = obj[cc];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        pc[u] = Pc[s0 + u];
-        pb[u] = Pb[s0 + u];
-      }
-#pragma unroll
-      for (int u = 0; u < 8 && s0 + u < KMAX; ++u) {
-        const int s = s0 + u;
-        if (s < q) {
-          fv = apply_pivot(fv, i, c, rls[s], cs[s], fs[s], pc[u], skip);
-          bv = apply_pivot(bv, i, rhs, rls[s], cs[s], fs[s], pb[u], skip);
-        }
-      }
-    }
+  for (int s = 0; s < KMAX; ++s) {
+    const bool act = s < q;
+    const bool isr = i == rdlane64(slot_r, s) - row0;
+    const bool isc = cc == rdlane64(slot_c, s);
+    fv = apply_sel(fv, isr, isc, act, fs[s], pc[s], skip);
+    bv = apply_sel(bv, isr, false, act, fs[s], pb[s], skip);  // the RHS never enters
   }
   SPX_PROBE(q, 0, 2, fv != 12345.678);
+  if (!go) return;
+  if (block0) {
+    st->c_next = c;
+    st->zc_next = zc;
+    st->n_ratio_part = gridDim.x * NWAVE;
+  }
   KeyR k = keyr_none();
   if (live) {
     win.F[(int64_t)q * ld + i] = fv;
     if (forced_c < 0) ratio_candidate(k, fv, bv, row0 + i, basis, rule, eps_piv);
   }
   if (forced_c < 0) {  // one partial per wave
-    wave_min(k);
-    if ((threadIdx.x & 63) == 0) store_key(ratio_part + blockIdx.x * NWAVE + (threadIdx.x >> 6), k);
+    wave_min_dpp(k);
+    if (lane == 0) store_key(ratio_part + blockIdx.x * NWAVE + (threadIdx.x >> 6), k);
   }
   SPX_PROBE(q, 0, 3, true);
 }
@@ -220,83 +249,90 @@ __global__ __launch_bounds__(BLK) void lazy_ratio_kernel(
 // for the next pivot, bookkeeping.  One thread per column; n_ratio = the
 // lazy_ratio partial count (a launch constant).  Both lazy kernels reduce and
 // publish per WAVE (every wave reduces all partials itself), so neither has a
-// block barrier on its critical path.
+// block barrier on its critical path.  Round trips as in lazy_ratio: (1) ratio
+// partials, this column's objective entry, tag and p_s values, the slots'
+// (r_s, c_s), state; (2) after the argmin, the stale row entry and the f_s
+// values of the leaving row.  The window's last slot (q == last) compacts the
+// touched columns into records for the flush, also when the window stopped.
 // ---------------------------------------------------------------------------
 template <int KMAX>
 __global__ __launch_bounds__(BLK) void lazy_norm_kernel(
-    const double* __restrict__ A, int64_t ld, int64_t m_local, int64_t row0, int64_t N,
-    double* __restrict__ obj, Window win, int q, int last, const Key* __restrict__ ratio_part,
-    int n_ratio, Key* __restrict__ enter_part, int64_t* __restrict__ basis,
-    int64_t* __restrict__ hist, const Params* __restrict__ prm, State* st) {
+    const Key* __restrict__ ratio_part, State* st, const Params* __restrict__ prm,
+    int n_ratio, int q, const double* __restrict__ A, int64_t ld, int64_t m_local,
+    int64_t row0, int64_t N, double* __restrict__ obj, Window win, int last,
+    Key* __restrict__ enter_part, int64_t* __restrict__ basis, int64_t* __restrict__ hist) {
+  static_assert(KMAX <= 64, "slots are lane-indexed");
   const bool block0 = blockIdx.x == 0 && threadIdx.x == 0;
   SPX_PROBE(q, 1, 0, true);
-  // independent loads first
+  const int lane = threadIdx.x & 63;
+  const int64_t j = (int64_t)blockIdx.x * BLK + threadIdx.x;
+  const bool live = j < N;
+  const int64_t jc = live ? j : 0;
+  // --- batch 1 ---
+  Keys8 kk;
+  keys_issue(kk, ratio_part, n_ratio);
+  asm volatile("" ::: "memory");  // the keys first (see lazy_ratio)
+  double o = obj[jc];
+  const uint32_t old = live ? win.tag[jc] : 0u;
+  double ps[KMAX];
+  const double* __restrict__ Pj = win.P + jc * KW;
+#pragma unroll
+  for (int s = 0; s < KMAX; s += 2) {
+    const dbl2 pp = ld2<false>(Pj + s);
+    ps[s] = pp.x;
+    ps[s + 1] = pp.y;
+  }
+  const int64_t slot_r = win.r[lane < KMAX ? lane : 0];
+  const int64_t slot_c = win.c[lane < KMAX ? lane : 0];
   const int32_t status = st->status;
   const int64_t c = st->c_next;
   const int64_t forced_r = st->forced_r;
-  const int64_t it = st->iters + q;  // iters only changes in flush_kernel
+  const int64_t it = st->iters + q;  // iters only changes in the flush
   const double zc = st->zc_next;
+  const int64_t hist_cap = st->hist_cap;
   const uint32_t epoch = *win.epoch & TAG_EPOCH;
   const int32_t rule = prm->rule;
   const double eps_opt = prm->eps_opt;
   const int64_t n_enter = prm->n_enter;
   const int64_t iter_limit = prm->iter_limit;
   const bool skip = prm->skip_zero != 0;
-  KeyR rk = lane_keys(ratio_part, n_ratio);  // per wave, of the per-wave ratio partials
-  const int64_t j = (int64_t)blockIdx.x * BLK + threadIdx.x;
-  const bool live = j < N;
-  double o = live ? obj[j] : 0.0;
-  const uint32_t old = live ? win.tag[j] : 0u;
-  double ps[KMAX];
-  int64_t rls[KMAX], cs[KMAX];
-  const double* __restrict__ Pj = win.P + (live ? j : 0) * KW;
-#pragma unroll
-  for (int s = 0; s < KMAX; s += 2) {  // unconditional: no load behind a slot branch
-    const dbl2 pp = ld2<false>(Pj + s);
-    ps[s] = pp.x;
-    ps[s + 1] = pp.y;
-  }
-#pragma unroll
-  for (int s = 0; s < KMAX; ++s) {
-    rls[s] = win.r[s] - row0;
-    cs[s] = win.c[s];
-  }
-  // stop: no pivot in this slot (grid-uniform); the window's last slot still
-  // compacts the columns the earlier slots touched
+  KeyR rk = keys_reduce(kk, ratio_part, n_ratio);
+  wave_min_dpp(rk);
+  // stop: no pivot in this slot (grid-uniform)
   bool stop = status != ST_RUNNING;
+  int32_t new_status = ST_RUNNING;
   if (!stop && (c < 0 || (forced_r < 0 && it >= iter_limit))) {
-    if (block0) st->status = (c < 0) ? ST_OPTIMAL : ST_LIMIT;
+    new_status = (c < 0) ? ST_OPTIMAL : ST_LIMIT;
     stop = true;
   }
-  int64_t r = forced_r;
+  const int64_t r = (forced_r >= 0) ? forced_r : rk.row;
   if (!stop && r < 0) {
-    wave_min(rk);
-    if (rk.row < 0) {
-      if (block0) st->status = ST_UNBOUNDED;
-      stop = true;
-    }
-    r = rk.row;
+    new_status = ST_UNBOUNDED;
+    stop = true;
   }
-  if (stop && block0) win.made[q] = 0;
+  if (block0 && new_status != ST_RUNNING) st->status = new_status;
+  if (block0 && stop) win.made[q] = 0;
+  SPX_PROBE(q, 1, 1, !stop);
+  // --- batch 2 (row clamped, so the loads are unconditional) ---
+  const int64_t rl = stop ? 0 : r - row0;
+  double v = A[jc * ld + rl];
+  const double piv = win.F[(int64_t)q * ld + rl];
+  double fr[KMAX];
+#pragma unroll
+  for (int s = 0; s < KMAX; ++s) fr[s] = win.F[(int64_t)s * ld + rl];
+  bool zb = false;  // (skip on) some earlier p_s[j] of this window is zero
+#pragma unroll
+  for (int s = 0; s < KMAX; ++s) {
+    const bool act = s < q;
+    const bool isr = rl == rdlane64(slot_r, s) - row0;
+    const bool isc = jc == rdlane64(slot_c, s);
+    v = apply_sel(v, isr, isc, act, fr[s], ps[s], skip);
+    zb |= act && skip && ps[s] == 0.0;
+  }
+  SPX_PROBE(q, 1, 2, v != 12345.678);
   uint32_t tg = old;  // this column's tag after this slot
   double p = 0.0;
   if (!stop) {
-    SPX_PROBE(q, 1, 1, r >= 0);
-    const int64_t rl = r - row0;
-    const double piv = win.F[(int64_t)q * ld + rl];
-    double v = live ? A[j * ld + rl] : 0.0;
-#pragma unroll
-    for (int s0 = 0; s0 < KMAX; s0 += 8) {
-      if (s0 < q) {
-        double fr[8];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) fr[u] = win.F[(int64_t)(s0 + u) * ld + rl];
-#pragma unroll
-        for (int u = 0; u < 8 && s0 + u < KMAX; ++u)
-          if (s0 + u < q) v = apply_pivot(v, rl, j, rls[s0 + u], cs[s0 + u], fr[u], ps[s0 + u], skip);
-      }
-    }
-    SPX_PROBE(q, 1, 2, v != 12345.678);
     KeyR ek = keyr_none();
     if (live) {
       p = v / piv;
@@ -308,13 +344,9 @@ __global__ __launch_bounds__(BLK) void lazy_norm_kernel(
         o = msub(o, zc, p);
       }
       obj[j] = o;
-      // tag: touched in this window; SPECIAL if it entered, ZERO if (skip on) one
-      // of its p_s[j] so far is zero
+      // tag: touched in this window; SPECIAL if it entered, ZERO if (skip on)
+      // one of its p_s[j] so far is zero
       const bool tagged = (old & TAG_EPOCH) == epoch;
-      bool zb = false;
-#pragma unroll
-      for (int s = 0; s < KMAX; ++s)
-        if (s < q) zb |= skip && ps[s] == 0.0;
       if (nz) {
         tg = epoch | ((j == c || (tagged && (old & TAG_SPECIAL))) ? TAG_SPECIAL : 0u) |
              (zb ? TAG_ZERO : 0u);
@@ -324,8 +356,8 @@ __global__ __launch_bounds__(BLK) void lazy_norm_kernel(
       if (tg != old) win.tag[j] = tg;
       if (j < n_enter && o < -eps_opt) kmin(ek, (rule == RULE_BLAND) ? 0.0 : o, j, j);
     }
-    wave_min(ek);  // one entering partial per wave
-    if ((threadIdx.x & 63) == 0) store_key(enter_part + blockIdx.x * NWAVE + (threadIdx.x >> 6), ek);
+    wave_min_dpp(ek);  // one entering partial per wave
+    if (lane == 0) store_key(enter_part + blockIdx.x * NWAVE + (threadIdx.x >> 6), ek);
     if (block0) {
       st->r = r;
       st->c = c;
@@ -335,7 +367,7 @@ __global__ __launch_bounds__(BLK) void lazy_norm_kernel(
       win.c[q] = c;
       win.made[q] = 1;
       basis[r] = c;
-      if (it < st->hist_cap) {
+      if (it < hist_cap) {
         hist[2 * it] = r;
         hist[2 * it + 1] = c;
       }
@@ -348,7 +380,7 @@ __global__ __launch_bounds__(BLK) void lazy_norm_kernel(
     __shared__ int wcnt[NWAVE];
     __shared__ int base;
     const uint64_t bal = __ballot(mine);
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int w = threadIdx.x >> 6;
     if (lane == 0) wcnt[w] = __popcll(bal);
     __syncthreads();
     if (threadIdx.x == 0) {

@@ -118,6 +118,58 @@ __device__ __forceinline__ void wave_min(KeyR& k) {
   }
 }
 
+// The same wave argmin without LDS: DPP row rotations / quad permutes inside
+// each row of 16 lanes, then the gfx950 permlane swaps for lanes 16 and 32
+// apart.  Every lane receives the result.  (__shfl_xor is a ds_bpermute per
+// dword: six dependent LDS round trips, ~0.7 us on the lazy kernels' path.)
+template <int CTRL>
+__device__ __forceinline__ int64_t dpp64(int64_t x) {
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)(x & 0xffffffff), CTRL, 0xf, 0xf, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(x >> 32), CTRL, 0xf, 0xf, false);
+  return ((int64_t)hi << 32) | (uint32_t)lo;
+}
+template <int CTRL>
+__device__ __forceinline__ void kmin_dpp(KeyR& k) {
+  const double v = __longlong_as_double(dpp64<CTRL>(__double_as_longlong(k.v)));
+  const int64_t t = dpp64<CTRL>(k.t);
+  const int64_t row = dpp64<CTRL>(k.row);
+  kmin(k, v, t, row);
+}
+// partner value `d` lanes away (d = 16 or 32) from the permlane swap pair
+template <int D>
+__device__ __forceinline__ int64_t swap64(int64_t x) {
+  const unsigned lo = (unsigned)(x & 0xffffffff), hi = (unsigned)(x >> 32);
+  const bool upper = (threadIdx.x & D) != 0;
+  unsigned plo, phi;
+  if constexpr (D == 16) {
+    const auto a = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
+    const auto b = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+    plo = upper ? a[0] : a[1];
+    phi = upper ? b[0] : b[1];
+  } else {
+    const auto a = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
+    const auto b = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+    plo = upper ? a[0] : a[1];
+    phi = upper ? b[0] : b[1];
+  }
+  return ((int64_t)phi << 32) | plo;
+}
+template <int D>
+__device__ __forceinline__ void kmin_swap(KeyR& k) {
+  const double v = __longlong_as_double(swap64<D>(__double_as_longlong(k.v)));
+  const int64_t t = swap64<D>(k.t);
+  const int64_t row = swap64<D>(k.row);
+  kmin(k, v, t, row);
+}
+__device__ __forceinline__ void wave_min_dpp(KeyR& k) {
+  kmin_dpp<0x128>(k);  // row_ror:8
+  kmin_dpp<0x124>(k);  // row_ror:4
+  kmin_dpp<0x4E>(k);   // quad_perm [2,3,0,1]
+  kmin_dpp<0xB1>(k);   // quad_perm [1,0,3,2]
+  kmin_swap<16>(k);
+  kmin_swap<32>(k);
+}
+
 // Block-wide argmin; every thread receives the result.
 __device__ __forceinline__ KeyR block_min(KeyR k) {
   __shared__ double sv[NWAVE];

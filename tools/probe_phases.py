@@ -20,7 +20,8 @@ LIB = os.path.join(PKG, "simplex_amd", "lib", "libspx_probe.so")
 
 def build():
     cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC",
-           "-shared", "-ffp-contract=off", "-DSPX_PHASE_TIMING", "-o", LIB,
+           "-shared", "-ffp-contract=off", "-mllvm", "-amdgpu-kernarg-preload-count=8",
+           "-DSPX_PHASE_TIMING"] + (["-DSPX_PROBE_FINE"] if os.environ.get("SPX_PROBE_FINE") else []) + ["-o", LIB,
            os.path.join(PKG, "csrc", "spx_capi.hip"), "-lrccl"]
     subprocess.run(cmd, check=True)
 
@@ -71,6 +72,9 @@ def main():
                   f"  phase1 +{ph[1]-ph[0]:5.2f}  phase2 +{ph[2]-ph[1]:5.2f}"
                   f"  end +{ph[3]-ph[2]:5.2f}  total {ph[3]-ph[0]:5.2f}")
             prev_end = ph[3]
+            if kind == 0 and os.environ.get("SPX_PROBE_FINE"):
+                k0, k1 = us(t(q, 2, 0)), us(t(q, 2, 1))
+                print(f"       fine: keys reduced +{k0 - ph[0]:5.2f}  wave_min +{k1 - k0:5.2f}")
     f0, f1 = us(t(K, 2, 0)), us(t(K, 2, 1))
     print(f"flush entry {f0:8.2f} (+{f0 - prev_end:5.2f})  block-0 duration {f1 - f0:7.2f}")
     rch, G = ctypes.c_int(), ctypes.c_int()
