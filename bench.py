@@ -262,7 +262,8 @@ def main():
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBPS,
                          "traffic": traffic,
-                         "kernel": "spx::flush_kernel" if K else "spx::elim_kernel",
+                         "kernel": (("spx::flush_lds_kernel" if max(args.fv, 0) in (0, 6, 7)
+                                     else "spx::flush_kernel") if K else "spx::elim_kernel"),
                          "avg_launch_us": avg_ms * 1e3,
                          "alg_bytes_per_launch": alg_bytes,
                          "touched_cols_per_launch": cols_per_launch,

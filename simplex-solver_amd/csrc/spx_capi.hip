@@ -102,6 +102,8 @@ struct spx_ctx {
   Params* prm = nullptr;
   State* st = nullptr;
   State* h_st = nullptr;   // pinned mirror
+  State* h_poll = nullptr; // pinned [2]: State copies polled one chunk behind (spx_solve)
+  hipEvent_t ev_poll[2] = {nullptr, nullptr};
   int64_t hist_cap = 0;
 
   // launch geometry
@@ -653,6 +655,9 @@ int spx_create(spx_ctx** out, int device) {
   if (e == hipSuccess) e = hipMalloc(&ctx->prm, sizeof(Params));
   if (e == hipSuccess) e = hipMalloc(&ctx->st, sizeof(State));
   if (e == hipSuccess) e = hipHostMalloc(&ctx->h_st, sizeof(State), hipHostMallocDefault);
+  if (e == hipSuccess) e = hipHostMalloc(&ctx->h_poll, 2 * sizeof(State), hipHostMallocDefault);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->ev_poll[0], hipEventDisableTiming);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->ev_poll[1], hipEventDisableTiming);
   if (e != hipSuccess) {
     ctx->err = std::string("spx_create: ") + hipGetErrorString(e);
     *out = ctx;  // caller may read the error, then destroy
@@ -745,6 +750,9 @@ int spx_destroy(spx_ctx* ctx) {
   dfree(ctx->prm);
   dfree(ctx->st);
   if (ctx->h_st) (void)hipHostFree(ctx->h_st);
+  if (ctx->h_poll) (void)hipHostFree(ctx->h_poll);
+  for (hipEvent_t ev : ctx->ev_poll)
+    if (ev) (void)hipEventDestroy(ev);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;
   return SPX_OK;
@@ -909,14 +917,27 @@ int spx_solve(spx_ctx* ctx, const spx_opts* opts, spx_result* res) {
     if (rc) return rc;
   }
   int status = SPX_RUNNING;
-  for (;;) {
+  // Chunk i+1 is enqueued before chunk i's status is read (a pinned State copy
+  // per chunk, polled one chunk behind), so the stream never drains while the
+  // host looks.  The chunk after the terminating one only runs early-exiting
+  // launches: every kernel checks the device status first.
+  auto launch_chunk = [&](int64_t i) -> int {
     if (use_graph) {
       HIPC(hipGraphLaunch(ctx->gexec, ctx->stream));
-    } else if ((rc = enqueue_pivots(ctx, chunk, 0))) {
-      return rc;
+    } else {
+      const int r = enqueue_pivots(ctx, chunk, 0);
+      if (r) return r;
     }
-    if ((rc = pull_state(ctx))) return rc;
-    status = map_status(ctx->h_st->status);
+    HIPC(hipMemcpyAsync(ctx->h_poll + (i & 1), ctx->st, sizeof(State), hipMemcpyDeviceToHost,
+                        ctx->stream));
+    HIPC(hipEventRecord(ctx->ev_poll[i & 1], ctx->stream));
+    return SPX_OK;
+  };
+  if ((rc = launch_chunk(0))) return rc;
+  for (int64_t i = 0;; ++i) {
+    if ((rc = launch_chunk(i + 1))) return rc;
+    HIPC(hipEventSynchronize(ctx->ev_poll[i & 1]));
+    status = map_status(ctx->h_poll[i & 1].status);
     if (status != SPX_RUNNING) break;
     const double el =
         std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
@@ -925,6 +946,7 @@ int spx_solve(spx_ctx* ctx, const spx_opts* opts, spx_result* res) {
       break;
     }
   }
+  if ((rc = pull_state(ctx))) return rc;  // the final state (after the extra chunk)
   double z = 0.0;
   HIPC(hipMemcpyAsync(&z, ctx->obj + (ctx->N - 1), sizeof(double), hipMemcpyDeviceToHost,
                       ctx->stream));

@@ -25,10 +25,11 @@ from simplex_amd import synth  # noqa: E402
 from simplex_amd.engine import DeviceTableau  # noqa: E402
 
 
-def config2():
+def config2(window=0):
     m, n, seed = 1024, 2048, 20251207
     T, basis = synth.full_tableau("dense", m, n, seed)
     with DeviceTableau(0) as e:
+        e.set_window(window)
         e.load(T, basis)
         e.solve(max_iters=5)  # warm: graph build, first launches
         e.load(T, basis)
@@ -45,7 +46,8 @@ def config2():
     t0 = time.perf_counter()
     h = linprog(-c, A_ub=A, b_ub=b, bounds=[(0, None)] * n, method="highs-ds")
     highs_s = time.perf_counter() - t0
-    return {"config": "2: 1024x2048 dense LP, full Dantzig solve", "gpu_s": gpu_s,
+    return {"config": "2: 1024x2048 dense LP, full Dantzig solve", "window": window,
+            "gpu_s": gpu_s,
             "pivots": res.iters, "gpu_pivots_per_s": res.iters / gpu_s,
             "objective": res.objective, "highs_objective": -h.fun, "highs_s": highs_s,
             "highs_nit": int(h.nit), "cpu_oracle_s": cpu_s, "cpu_threads": C.threads(),
@@ -53,10 +55,11 @@ def config2():
             "objective_rel_err_vs_highs": abs(res.objective + h.fun) / abs(h.fun)}
 
 
-def config5(k=2000, k_cpu=60):
+def config5(window=0, k=2048, k_cpu=60):
     m = n = 4096
     T, basis = synth.full_tableau("degenerate", m, n, 5)
     with DeviceTableau(0) as e:
+        e.set_window(window)
         e.load(T, basis)
         e.run_pivots(20, rule="bland")
         e.sync()
@@ -70,12 +73,12 @@ def config5(k=2000, k_cpu=60):
     t0 = time.perf_counter()
     stc, hc = C.solve(Tc, bc, rule="bland", max_iters=k_cpu)
     cpu_s = time.perf_counter() - t0
-    return {"config": "5: degenerate 4096x4096 LP, Bland", "gpu_pivots": k,
+    return {"config": "5: degenerate 4096x4096 LP, Bland", "window": window, "gpu_pivots": k,
             "gpu_pivots_per_s": k / gpu_s, "status_after": st, "iters": it,
             "cpu_oracle_pivots_per_s": len(hc) / cpu_s, "cpu_threads": C.threads(),
             "first_pivots_match_oracle": [tuple(x) for x in hist[:len(hc)]] == hc}
 
 
 if __name__ == "__main__":
-    for fn in (config2, config5):
-        print(json.dumps(fn()), flush=True)
+    for fn, w in ((config2, 0), (config2, 8), (config2, 16), (config5, 0), (config5, 16)):
+        print(json.dumps(fn(w)), flush=True)

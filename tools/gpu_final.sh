@@ -15,6 +15,6 @@ step() { local lim=$1 log=$2; shift 2
 [ "${DO_CFG:-1}" != 0 ] && TAILN=2 step 600 bench_configs.log python tools/bench_configs.py
 step 400 bench.log python bench.py --cpu-seconds 15
 step 400 rocprof_stats.log rocprofv3 --kernel-trace --stats -d gpurun_out/final/prof -o bench --output-format csv -- python3 bench.py --cpu-seconds 0
-step 400 pmc_fetch.log rocprofv3 --pmc FETCH_SIZE -d gpurun_out/final/pmc_fetch -o f --output-format csv -- python3 bench.py --steps 40 --warmup 5 --cpu-seconds 0
-step 400 pmc_write.log rocprofv3 --pmc WRITE_SIZE -d gpurun_out/final/pmc_write -o w --output-format csv -- python3 bench.py --steps 40 --warmup 5 --cpu-seconds 0
+step 400 pmc_fetch.log rocprofv3 --pmc FETCH_SIZE -d gpurun_out/final/pmc_fetch -o f --output-format csv -- python3 bench.py --steps 128 --warmup 16 --cpu-seconds 0
+step 400 pmc_write.log rocprofv3 --pmc WRITE_SIZE -d gpurun_out/final/pmc_write -o w --output-format csv -- python3 bench.py --steps 128 --warmup 16 --cpu-seconds 0
 exit 0

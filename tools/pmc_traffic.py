@@ -25,7 +25,7 @@ def main():
     fcsv, wcsv, key, m_local, cols, out = sys.argv[1:7]
     K = float(sys.argv[7]) if len(sys.argv) > 7 else 0.0
     m_local, cols = int(m_local), float(cols)
-    match = "flush_kernel" if K > 1 else "elim_kernel"
+    match = "flush_" if K > 1 else "elim_kernel"  # flush_kernel or flush_lds_kernel
     f_kib, nf = per_dispatch(fcsv, "FETCH_SIZE", match)
     w_kib, nw = per_dispatch(wcsv, "WRITE_SIZE", match)
     fetch = 2.0 * f_kib * 1024.0
