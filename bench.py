@@ -28,7 +28,7 @@ sys.path.insert(0, ROOT)
 import numpy as np  # noqa: E402
 
 METRIC = "pivots/sec + row-elim HBM GB/s (% roofline), fp64 dense tableau, 1/2/4/8 GPU"
-DEFAULT_WINDOW = 16  # windowed elimination on one GPU
+DEFAULT_WINDOW = 24  # windowed elimination on one GPU (K sweep in profiles/r01)
 HBM_PEAK_GBPS = 8000.0  # MI355X spec HBM3E peak (MI355X_MICROARCH.md)
 
 

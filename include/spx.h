@@ -173,8 +173,8 @@ int spx_set_elim_variant(spx_ctx* ctx, int R, int target_wgs, int nt_flags, int 
  * interleave, pipelining, leading dimension. */
 int spx_get_elim_variant(const spx_ctx* ctx, int64_t out[7]);
 /* Windowed ("delayed") elimination: apply K pivots per streaming pass over
- * the tableau (2..16; 0 or 1 = one pass per pivot).  Results are bit-identical
- * (DESIGN.md §4).  Single-GPU contexts only. */
+ * the tableau (K in 2, 4, 8, 12, 16, 24, 32; 0 or 1 = one pass per pivot).
+ * Results are bit-identical.  Single-GPU contexts only. */
 int spx_set_window(spx_ctx* ctx, int K);
 /* Layout knob: extra doubles of padding per stored column (even, 0..4096);
   * applies to the next spx_load / spx_load_rows; -1 = automatic. */

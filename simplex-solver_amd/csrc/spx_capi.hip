@@ -113,7 +113,7 @@ struct spx_ctx {
   int elim_ilv = 1;        // interleaved column assignment
   int elim_pipe = 1;       // software-pipelined column pairs (+12% on config 3)
   int elim_xcd = 0;        // XCD-aware block swizzle
-  int flush_bpc[5 * 8] = {};  // resident flush blocks per CU, by (window 2..32, variant); 0 unknown
+  int flush_bpc[7 * 8] = {};  // resident flush blocks per CU, by (window size, variant); 0 unknown
   int flush_var = 0;       // flush kernel variant (rows per thread x columns per step)
   int last_flush_G = 0;    // column groups of the last flush launch
   int n_cu = 0;
@@ -382,8 +382,8 @@ int enqueue_window_t(spx_ctx* ctx, int npiv, bool time_flush) {
     const int rc = record_event(ctx, e->first);
     if (rc) return rc;
   }
-  const int slot = (KMAX == 2 ? 0 : KMAX == 4 ? 1 : KMAX == 8 ? 2 : KMAX == 16 ? 3 : 4) +
-                   5 * ctx->flush_var;
+  const int slot = (KMAX == 2 ? 0 : KMAX == 4 ? 1 : KMAX == 8 ? 2 : KMAX == 12 ? 3
+                    : KMAX == 16 ? 4 : KMAX == 24 ? 5 : 6) + 7 * ctx->flush_var;
   auto go = [&](auto kern, int rt) {
     const int rch = flush_rch(ctx, rt);
     const int G = flush_groups(ctx, slot, (const void*)kern, rch);
@@ -397,12 +397,14 @@ int enqueue_window_t(spx_ctx* ctx, int npiv, bool time_flush) {
   // compacted records; 6 / 7 the same with rings of 9 / 16; register rings
   // (rows per lane x depth, A = sweep direction alternating per window):
   // 1 2x4, 2 4x4, 3 4x4A, 4 2x8, 5 2x4A (profiles/r01/tune_flush_*.log)
-  switch (ctx->flush_var) {
-    case 1: nts ? go(flush_kernel<KMAX, 2, 4, true>, 2) : go(flush_kernel<KMAX, 2, 4, false>, 2); break;
-    case 2: nts ? go(flush_kernel<KMAX, 4, 4, true>, 4) : go(flush_kernel<KMAX, 4, 4, false>, 4); break;
-    case 3: nts ? go(flush_kernel<KMAX, 4, 4, true, true>, 4) : go(flush_kernel<KMAX, 4, 4, false, true>, 4); break;
-    case 4: nts ? go(flush_kernel<KMAX, 2, 8, true>, 2) : go(flush_kernel<KMAX, 2, 8, false>, 2); break;
-    case 5: nts ? go(flush_kernel<KMAX, 2, 4, true, true>, 2) : go(flush_kernel<KMAX, 2, 4, false, true>, 2); break;
+  // (register rings exist for power-of-two windows only; others take the default)
+  constexpr bool POW2 = (KMAX & (KMAX - 1)) == 0;
+  switch (POW2 ? ctx->flush_var : 0) {
+    case 1: if constexpr (POW2) { nts ? go(flush_kernel<KMAX, 2, 4, true>, 2) : go(flush_kernel<KMAX, 2, 4, false>, 2); } break;
+    case 2: if constexpr (POW2) { nts ? go(flush_kernel<KMAX, 4, 4, true>, 4) : go(flush_kernel<KMAX, 4, 4, false>, 4); } break;
+    case 3: if constexpr (POW2) { nts ? go(flush_kernel<KMAX, 4, 4, true, true>, 4) : go(flush_kernel<KMAX, 4, 4, false, true>, 4); } break;
+    case 4: if constexpr (POW2) { nts ? go(flush_kernel<KMAX, 2, 8, true>, 2) : go(flush_kernel<KMAX, 2, 8, false>, 2); } break;
+    case 5: if constexpr (POW2) { nts ? go(flush_kernel<KMAX, 2, 4, true, true>, 2) : go(flush_kernel<KMAX, 2, 4, false, true>, 2); } break;
     case 6: nts ? go(flush_lds_kernel<KMAX, 9, true>, 2) : go(flush_lds_kernel<KMAX, 9, false>, 2); break;
     case 7: nts ? go(flush_lds_kernel<KMAX, 16, true>, 2) : go(flush_lds_kernel<KMAX, 16, false>, 2); break;
     default: nts ? go(flush_lds_kernel<KMAX, 12, true>, 2) : go(flush_lds_kernel<KMAX, 12, false>, 2);
@@ -424,7 +426,9 @@ int enqueue_window(spx_ctx* ctx, int npiv, bool time_flush) {
     case 2: return enqueue_window_t<2>(ctx, npiv, time_flush);
     case 4: return enqueue_window_t<4>(ctx, npiv, time_flush);
     case 8: return enqueue_window_t<8>(ctx, npiv, time_flush);
+    case 12: return enqueue_window_t<12>(ctx, npiv, time_flush);
     case 16: return enqueue_window_t<16>(ctx, npiv, time_flush);
+    case 24: return enqueue_window_t<24>(ctx, npiv, time_flush);
     default: return enqueue_window_t<32>(ctx, npiv, time_flush);
   }
 }
@@ -1066,8 +1070,9 @@ int spx_probe_flush_grid(spx_ctx* ctx, int* rch, int* G) {
 
 int spx_set_window(spx_ctx* ctx, int K) {
   if (!ctx) return SPX_E_ARG;
-  CHECK_ARG(K == 0 || K == 1 || K == 2 || K == 4 || K == 8 || K == 16 || K == 32,
-            "window must be 0, 1, 2, 4, 8, 16 or 32");
+  CHECK_ARG(K == 0 || K == 1 || K == 2 || K == 4 || K == 8 || K == 12 || K == 16 || K == 24 ||
+                K == 32,
+            "window must be 0, 1, 2, 4, 8, 12, 16, 24 or 32");
   CHECK_ARG(K <= 1 || !ctx->sharded, "windowed elimination is single-GPU only");
   ctx->win_k = K <= 1 ? 0 : K;
   drop_graphs(ctx);
