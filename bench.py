@@ -35,8 +35,10 @@ HBM_PEAK_GBPS = 8000.0  # MI355X spec HBM3E peak (MI355X_MICROARCH.md)
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=500)
-    ap.add_argument("--warmup", type=int, default=20)
+    # defaults: whole windows of the default K (a partial window's flush is a
+    # separate, slower code path -- every slot guarded)
+    ap.add_argument("--steps", type=int, default=480)
+    ap.add_argument("--warmup", type=int, default=48)
     ap.add_argument("--m", type=int, default=8192)
     ap.add_argument("--n", type=int, default=8192)
     ap.add_argument("--seed", type=int, default=20251205)

@@ -407,15 +407,19 @@ int enqueue_window_t(spx_ctx* ctx, int npiv, bool time_flush) {
     case 5: if constexpr (POW2) { nts ? go(flush_kernel<KMAX, 2, 4, true, true>, 2) : go(flush_kernel<KMAX, 2, 4, false, true>, 2); } break;
     case 6: nts ? go(flush_lds_kernel<KMAX, 9, true>, 2) : go(flush_lds_kernel<KMAX, 9, false>, 2); break;
     case 7: nts ? go(flush_lds_kernel<KMAX, 16, true>, 2) : go(flush_lds_kernel<KMAX, 16, false>, 2); break;
-    default: nts ? go(flush_lds_kernel<KMAX, 12, true>, 2) : go(flush_lds_kernel<KMAX, 12, false>, 2);
+    default:
+      if (npiv < KMAX)  // the last window of a request: every slot guarded
+        nts ? go(flush_lds_kernel<KMAX, 12, true, true>, 2) : go(flush_lds_kernel<KMAX, 12, false, true>, 2);
+      else
+        nts ? go(flush_lds_kernel<KMAX, 12, true>, 2) : go(flush_lds_kernel<KMAX, 12, false>, 2);
   }
   if (e) {
     const int rc = record_event(ctx, e->second);
     if (rc) return rc;
   }
-  if (npiv == KMAX)  // full windows leave the fast-path columns' leaving rows to it
-    hipLaunchKernelGGL(row_fix_kernel<KMAX>, dim3(ctx->nbn), dim3(BLK), 0, ctx->stream, ctx->A,
-                       ctx->ld, ctx->m_local, ctx->row0, ctx->N, ctx->win);
+  // the fast-path columns' leaving rows (every window: partial ones included)
+  hipLaunchKernelGGL(row_fix_kernel<KMAX>, dim3(ctx->nbn), dim3(BLK), 0, ctx->stream, ctx->A,
+                       ctx->ld, ctx->m_local, ctx->row0, ctx->N, ctx->win, npiv);
   HIPC(hipGetLastError());
   return SPX_OK;
 }

@@ -695,7 +695,7 @@ __device__ __forceinline__ void wait_vmcnt() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-template <int K, int D, bool NTS>
+template <int K, int D, bool NTS, bool PART = false>
 __global__ __launch_bounds__(BLK) void flush_lds_kernel(double* __restrict__ A, int64_t ld,
                                                         int64_t m_local, int64_t row0,
                                                         int64_t N, Window win, int npiv,
@@ -774,12 +774,26 @@ __global__ __launch_bounds__(BLK) void flush_lds_kernel(double* __restrict__ A, 
     dbl2 x = ring[(w * D + slot) * 64 + lane];
     auto pv = [&](int s) -> double { return pc[s]; };
     const int64_t j = hc & 0xffffffffll;
-    const bool fast = full && (hc >> 32) == 0;
-    if (fast) {
+    if ((hc >> 32) == 0 && (PART || full)) {
+      // fast path: the straight msub chain over the made slots, leaving rows
+      // included (row_fix_kernel rewrites those).  PART: the instance launched
+      // for a window of fewer than K pivots guards each slot (a separate
+      // instance: the guards cost the full-window loop its register budget);
+      // a full-size window that stopped early takes the exact path below
+      if constexpr (!PART) {
 #pragma unroll
-      for (int s = 0; s < K; ++s) {
-        x.x = msub(x.x, f[s][0], pv(s));
-        x.y = msub(x.y, f[s][1], pv(s));
+        for (int s = 0; s < K; ++s) {
+          x.x = msub(x.x, f[s][0], pv(s));
+          x.y = msub(x.y, f[s][1], pv(s));
+        }
+      } else {
+#pragma unroll
+        for (int s = 0; s < K; ++s) {
+          if (s < nm) {
+            x.x = msub(x.x, f[s][0], pv(s));
+            x.y = msub(x.y, f[s][1], pv(s));
+          }
+        }
       }
     } else {
       // (r_s, c_s) reloaded on this rare path: the laundered bases keep the
@@ -817,8 +831,8 @@ __global__ __launch_bounds__(BLK) void flush_lds_kernel(double* __restrict__ A, 
 }
 
 // ---------------------------------------------------------------------------
-// row_fix_kernel<K>: after a FULL window's flush, rewrite the leaving rows of
-// the fast-path columns (tagged, not SPECIAL / ZERO).  For such a column no
+// row_fix_kernel<K>: after a window's flush (its made slots: a prefix of K),
+// rewrite the leaving rows of the fast-path columns (tagged, not SPECIAL / ZERO).  For such a column no
 // pivot of the window enters it and every p_s[j] != 0, so a leaving row r
 // whose last leaving slot is L ends at p_L[j] followed by the later pivots'
 // msub updates (their leaving rows differ from r).  One thread per column.
@@ -826,7 +840,7 @@ __global__ __launch_bounds__(BLK) void flush_lds_kernel(double* __restrict__ A, 
 template <int K>
 __global__ __launch_bounds__(BLK) void row_fix_kernel(double* __restrict__ A, int64_t ld,
                                                       int64_t m_local, int64_t row0, int64_t N,
-                                                      Window win) {
+                                                      Window win, int npiv) {
   __shared__ double fr[K][K];  // fr[L][s] = f_s[r_L]
   __shared__ int64_t rows[K];
   __shared__ int lastL[K];
@@ -835,8 +849,8 @@ __global__ __launch_bounds__(BLK) void row_fix_kernel(double* __restrict__ A, in
   const bool live = j < N;
   const uint32_t tg = live ? win.tag[j] : 0u;
   const uint32_t epoch = *win.epoch & TAG_EPOCH;
-  int madeK = 0;
-  for (int s = 0; s < K; ++s) madeK += win.made[s];
+  int madeK = 0;  // made slots of this window: a prefix of its npiv launched ones
+  for (int s = 0; s < npiv; ++s) madeK += win.made[s];
   double p[K];
 #pragma unroll
   for (int s = 0; s < K; ++s) p[s] = win.P[(live ? j : 0) * KW + s];
@@ -849,20 +863,21 @@ __global__ __launch_bounds__(BLK) void row_fix_kernel(double* __restrict__ A, in
   }
   if (threadIdx.x < K) {
     const int64_t r = win.r[threadIdx.x];
-    bool last = true;
-    for (int s = threadIdx.x + 1; s < K; ++s) last &= win.r[s] != r;
+    bool last = true;  // the last leaving slot of row r among the made ones
+    for (int s = threadIdx.x + 1; s < madeK; ++s) last &= win.r[s] != r;
     rows[threadIdx.x] = r - row0;
     lastL[threadIdx.x] = last;
   }
   __syncthreads();
-  if (madeK != K || !live || (tg & TAG_EPOCH) != epoch || (tg & (TAG_SPECIAL | TAG_ZERO)))
+  if (madeK == 0 || !live || (tg & TAG_EPOCH) != epoch || (tg & (TAG_SPECIAL | TAG_ZERO)))
     return;
 #pragma unroll
   for (int L = 0; L < K; ++L) {
-    if (!lastL[L]) continue;
+    if (L >= madeK || !lastL[L]) continue;
     double x = p[L];
 #pragma unroll
-    for (int s = L + 1; s < K; ++s) x = msub(x, fr[L][s], p[s]);
+    for (int s = L + 1; s < K; ++s)
+      if (s < madeK) x = msub(x, fr[L][s], p[s]);
     A[j * ld + rows[L]] = x;
   }
 }

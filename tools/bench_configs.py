@@ -80,5 +80,5 @@ def config5(window=0, k=2048, k_cpu=60):
 
 
 if __name__ == "__main__":
-    for fn, w in ((config2, 0), (config2, 8), (config2, 16), (config5, 0), (config5, 16)):
+    for fn, w in ((config2, 0), (config2, 8), (config2, 24), (config5, 0), (config5, 16), (config5, 24)):
         print(json.dumps(fn(w)), flush=True)

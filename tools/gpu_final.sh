@@ -17,4 +17,6 @@ step 400 bench.log python bench.py --cpu-seconds 15
 step 400 rocprof_stats.log rocprofv3 --kernel-trace --stats -d gpurun_out/final/prof -o bench --output-format csv -- python3 bench.py --cpu-seconds 0
 step 400 pmc_fetch.log rocprofv3 --pmc FETCH_SIZE -d gpurun_out/final/pmc_fetch -o f --output-format csv -- python3 bench.py --steps 128 --warmup 16 --cpu-seconds 0
 step 400 pmc_write.log rocprofv3 --pmc WRITE_SIZE -d gpurun_out/final/pmc_write -o w --output-format csv -- python3 bench.py --steps 128 --warmup 16 --cpu-seconds 0
+
+step 120 smoke.log python -c "import __graft_entry__ as g; g.smoke()"
 exit 0
