@@ -67,12 +67,28 @@ def make_opts(rule="dantzig", eps_opt=1e-9, eps_piv=1e-12, max_iters=0, time_lim
     return o
 
 
+def auto_window(m: int, cols: int) -> int:
+    """Window size (pivots per tableau pass) for a solve to
+    optimality on an m x cols constraint block: none for small tableaux (the
+    single-pivot path is launch-bound there either way), 8 from ~1M cells,
+    16 from ~8M, 24 from ~64M (profiles/r01/bench_configs.jsonl, bench K sweep)."""
+    cells = int(m) * int(cols)
+    if cells < (1 << 20):
+        return 0
+    if cells < (1 << 23):
+        return 8
+    if cells < (1 << 26):
+        return 16
+    return 24
+
+
 class DeviceTableau:
     """A tableau resident on one GPU (or one row shard of it, see dist.py)."""
 
     def __init__(self, device: int = 0, *, _sharded=None):
         self._lib = L.lib()
         self._ctx = ctypes.c_void_p()
+        self.sharded = _sharded is not None  # row shards reject windows (spx_set_window)
         if _sharded is None:
             rc = self._lib.spx_create(ctypes.byref(self._ctx), int(device))
         else:

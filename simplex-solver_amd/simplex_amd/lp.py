@@ -31,7 +31,7 @@ from typing import Callable, List, Optional, Sequence
 
 import numpy as np
 
-from .engine import DeviceTableau, SolveResult
+from .engine import DeviceTableau, SolveResult, auto_window
 from . import _lib as L
 
 OPS = {"<=": "L", "L": "L", ">=": "G", "G": "G", "=": "E", "==": "E", "E": "E"}
@@ -175,9 +175,10 @@ class _Recorder:
 
 
 def _run_phase(eng: DeviceTableau, rec: _Recorder, phase: int, rule: str, n_enter: int,
-               max_iters: int, time_limit: float, pivots: list) -> SolveResult:
+               max_iters: int, time_limit: float, pivots: list, window: int = 0) -> SolveResult:
     """Pivot until optimal/unbounded/limit.  Snapshots one pivot at a time
-    while the recorder's budget lasts, then hands the rest to spx_solve."""
+    while the recorder's budget lasts, then hands the rest to spx_solve, in
+    K-pivot windows when `window` > 1 (bit-identical)."""
     done = 0
     while rec.snapshot_ok() and (max_iters <= 0 or done < max_iters):
         out = eng.pivot(rule=rule, n_enter=n_enter)
@@ -191,9 +192,15 @@ def _run_phase(eng: DeviceTableau, rec: _Recorder, phase: int, rule: str, n_ente
         st, _, z = eng.state()
         return SolveResult(L.SPX_ITER_LIMIT, done, z, 0.0)
     before = eng.history().shape[0]
-    res = eng.solve(rule=rule, n_enter=n_enter,
-                    max_iters=(max_iters - done) if max_iters > 0 else 0,
-                    time_limit=time_limit)
+    if window > 1:
+        eng.set_window(window)
+    try:
+        res = eng.solve(rule=rule, n_enter=n_enter,
+                        max_iters=(max_iters - done) if max_iters > 0 else 0,
+                        time_limit=time_limit)
+    finally:
+        if window > 1:
+            eng.set_window(0)
     hist = eng.history()
     for r, c in hist[before:]:
         pivots.append((phase, int(r), int(c)))
@@ -209,10 +216,14 @@ def _run_phase(eng: DeviceTableau, rec: _Recorder, phase: int, rule: str, n_ente
 
 def solve_standard_form(sf: StandardForm, *, device: int = 0, rule: str = "dantzig",
                         max_iters: int = 0, time_limit: float = 0.0, record: bool = False,
-                        cell_budget: int = 2_000_000,
+                        cell_budget: int = 2_000_000, window: int = -1,
                         engine_factory: Optional[Callable[[], DeviceTableau]] = None) -> LPResult:
-    """Two-phase tableau simplex of a StandardForm on the GPU engine."""
+    """Two-phase tableau simplex of a StandardForm on the GPU engine.
+    window: pivots per tableau pass for the unrecorded stretch of each phase
+    (-1: auto_window by size; 0: one pass per pivot)."""
     eng = engine_factory() if engine_factory else DeviceTableau(device)
+    if window < 0:
+        window = 0 if getattr(eng, "sharded", False) else auto_window(sf.m, sf.N)
     try:
         eng.load(sf.T, sf.basis)
         rec = _Recorder(eng, record, cell_budget)
@@ -220,7 +231,8 @@ def solve_standard_form(sf: StandardForm, *, device: int = 0, rule: str = "dantz
         pivots: list = []
         iters = 0
         if sf.k:
-            res = _run_phase(eng, rec, 1, rule, sf.n_enter, max_iters, time_limit, pivots)
+            res = _run_phase(eng, rec, 1, rule, sf.n_enter, max_iters, time_limit, pivots,
+                             window)
             iters += res.iters
             if res.status == L.SPX_ITER_LIMIT:
                 return LPResult(L.SPX_ITER_LIMIT, None, None, iters, eng.basis(), pivots,
@@ -244,7 +256,8 @@ def solve_standard_form(sf: StandardForm, *, device: int = 0, rule: str = "dantz
             eng.set_phase2_objective(sf.cost)  # == phase2_objective(T, basis, cost)
             rec.record(None, None, 2)
         res = _run_phase(eng, rec, 2, rule, sf.n_enter,
-                         (max_iters - iters) if max_iters > 0 else 0, time_limit, pivots)
+                         (max_iters - iters) if max_iters > 0 else 0, time_limit, pivots,
+                         window)
         iters += res.iters
         if rec.enabled and rec.steps and not rec.steps[-1]["tableau"]:
             rec.steps[-1]["tableau"] = eng.tableau().tolist()

@@ -276,3 +276,33 @@ def test_window_config3_size_matches_single_pivot_path(eng_cls):
         s.solve(max_iters=48)
         assert s.history().tolist() == hw
         assert s.tableau().tobytes() == tw.tobytes()
+
+
+def test_two_phase_driver_auto_window_matches_single_pivot():
+    """lp.solve_standard_form picks K-pivot windows by size (auto_window: 8 at
+    this ~1.3M-cell tableau); phase 1, drive-out and phase 2 give the exact
+    pivot sequence, point and objective of the single-pivot engine."""
+    from simplex_amd import lp
+    from simplex_amd.engine import auto_window
+    rng = np.random.default_rng(11)
+    m, n = 600, 1300
+    rows = []
+    for i in range(m):
+        a = rng.uniform(0.05, 1.0, size=n)
+        a[rng.random(n) < 0.2] = 0.0
+        if i % 7 == 0:
+            rows.append((a.tolist(), ">=", float(rng.uniform(1, 5))))
+        elif i % 11 == 0:
+            rows.append((a.tolist(), "=", float(rng.uniform(20, 40))))
+        else:
+            rows.append((a.tolist(), "<=", float(rng.uniform(50, 100))))
+    c = rng.uniform(0.1, 1.0, size=n).tolist()
+    sf = lp.build_standard_form(c, rows, maximize=True)
+    assert sf.k > 0 and auto_window(sf.m, sf.N) == 8
+    r_auto = lp.solve_standard_form(sf)
+    r_one = lp.solve_standard_form(sf, window=0)
+    assert r_auto.status == r_one.status
+    assert r_auto.pivots == r_one.pivots and r_auto.iters == r_one.iters
+    if r_one.status == 0:
+        assert r_auto.objective == r_one.objective
+        assert np.array_equal(r_auto.x, r_one.x)

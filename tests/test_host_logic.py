@@ -182,3 +182,15 @@ def test_storage_service_writes_unique_files(tmp_path, monkeypatch):
     a = storage.StorageService.save_solution({"a": np.float64(1.5), "t": (1, 2)})
     b = storage.StorageService.save_solution({"b": 2})
     assert a != b and a.endswith("solucion_1.json") and b.endswith("solucion_2.json")
+
+
+def test_auto_window_by_size():
+    """The two-phase driver's window choice: off for small
+    tableaux, growing with the cell count; always a size spx_set_window takes."""
+    from simplex_amd.engine import auto_window
+    assert auto_window(3, 7) == 0
+    assert auto_window(1024, 3073) == 8          # config 2
+    assert auto_window(4096, 8193) == 16         # config 5
+    assert auto_window(8192, 16385) == 24        # config 3
+    for m, n in ((0, 0), (10, 10), (2000, 600), (5000, 20000), (100000, 200000)):
+        assert auto_window(m, n) in (0, 8, 16, 24)
