@@ -57,7 +57,7 @@ def parse():
     ap.add_argument("--ld-pad", type=int, default=-1, help="column padding (doubles)")
     ap.add_argument("--window", type=int, default=-1,
                     help="windowed elimination: K pivots per tableau pass (0 = off, "
-                         "-1 = default: %d on one GPU, off when sharded)" % DEFAULT_WINDOW)
+                         "-1 = default: %d, on one GPU and on row shards)" % DEFAULT_WINDOW)
     ap.add_argument("--time-every", type=int, default=0,
                     help="HIP events around every k-th elimination (or window flush) of the "
                          "timed region (0: 8 eliminations / 4 flushes; an event node costs "
@@ -164,7 +164,7 @@ def main():
         eng.set_ld_pad(args.ld_pad)
     row0, row1 = row_partition(m, world, rank)
     Tf, obj, basis = synth.tableau_rows("dense", m, n, args.seed, row0, row1, order="F")
-    K = args.window if args.window >= 0 else (DEFAULT_WINDOW if world == 1 else 0)
+    K = args.window if args.window >= 0 else DEFAULT_WINDOW
     K = 0 if K <= 1 else K
     if K:
         eng.set_window(K)

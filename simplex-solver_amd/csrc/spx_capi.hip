@@ -353,7 +353,9 @@ int flush_groups(spx_ctx* ctx, int slot, const void* kern, int rch) {
   return std::max(1, ctx->flush_bpc[slot] * ctx->n_cu / rch);
 }
 // lazy_ratio grid: one row per thread
-int lazy_ratio_grid(const spx_ctx* ctx) { return (int)((ctx->m_local + BLK - 1) / BLK); }
+int lazy_ratio_grid(const spx_ctx* ctx) {
+  return std::max(1, (int)((ctx->m_local + BLK - 1) / BLK));
+}
 
 template <int KMAX>
 int enqueue_window_t(spx_ctx* ctx, int npiv, bool time_flush) {
@@ -364,11 +366,29 @@ int enqueue_window_t(spx_ctx* ctx, int npiv, bool time_flush) {
                        NWAVE * ctx->nbn, q, (const double*)ctx->A, ctx->ld, ctx->m_local,
                        ctx->row0, ctx->N, (const double*)ctx->obj, ctx->win, ctx->ratio_part,
                        (const int64_t*)ctx->basis);
-    hipLaunchKernelGGL(lazy_norm_kernel<KMAX>, dim3(ctx->nbn), dim3(BLK), 0, ctx->stream,
-                       (const Key*)ctx->ratio_part, ctx->st, (const Params*)ctx->prm,
-                       NWAVE * nbw, q, (const double*)ctx->A, ctx->ld, ctx->m_local,
-                       ctx->row0, ctx->N, ctx->obj, ctx->win, npiv - 1, ctx->enter_part,
-                       ctx->basis, ctx->hist);
+    if (!ctx->sharded) {
+      hipLaunchKernelGGL(lazy_norm_kernel<KMAX>, dim3(ctx->nbn), dim3(BLK), 0, ctx->stream,
+                         (const Key*)ctx->ratio_part, ctx->st, (const Params*)ctx->prm,
+                         NWAVE * nbw, q, (const double*)ctx->A, ctx->ld, ctx->m_local,
+                         ctx->row0, ctx->N, ctx->obj, ctx->win, npiv - 1, ctx->enter_part,
+                         ctx->basis, ctx->hist, nullptr, (int64_t)0, 0);
+    } else {
+      // row shard: local candidate row (current values) -> ONE all-gather of
+      // [key | p] -> every rank takes the winner's p
+      hipLaunchKernelGGL(lazy_prep_kernel<KMAX>, dim3(ctx->nbn), dim3(BLK), 0, ctx->stream,
+                         (const Key*)ctx->ratio_part, (const State*)ctx->st,
+                         (const Params*)ctx->prm, NWAVE * nbw, q, (const double*)ctx->A,
+                         ctx->ld, ctx->m_local, ctx->row0, ctx->N, ctx->win, ctx->sendbuf,
+                         ctx->rank);
+      const int rc = comm_allgather(ctx);
+      if (rc) return rc;
+      hipLaunchKernelGGL((lazy_norm_kernel<KMAX, true>), dim3(ctx->nbn), dim3(BLK), 0,
+                         ctx->stream, (const Key*)ctx->ratio_part, ctx->st,
+                         (const Params*)ctx->prm, NWAVE * nbw, q, (const double*)ctx->A,
+                         ctx->ld, ctx->m_local, ctx->row0, ctx->N, ctx->obj, ctx->win,
+                         npiv - 1, ctx->enter_part, ctx->basis, ctx->hist,
+                         (const char*)ctx->recvbuf, ctx->gstride, ctx->nranks);
+    }
   }
   std::pair<hipEvent_t, hipEvent_t>* e = nullptr;
   if (time_flush) {
@@ -1077,7 +1097,6 @@ int spx_set_window(spx_ctx* ctx, int K) {
   CHECK_ARG(K == 0 || K == 1 || K == 2 || K == 4 || K == 8 || K == 12 || K == 16 || K == 24 ||
                 K == 32,
             "window must be 0, 1, 2, 4, 8, 12, 16, 24 or 32");
-  CHECK_ARG(K <= 1 || !ctx->sharded, "windowed elimination is single-GPU only");
   ctx->win_k = K <= 1 ? 0 : K;
   drop_graphs(ctx);
   return SPX_OK;

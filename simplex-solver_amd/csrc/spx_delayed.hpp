@@ -281,12 +281,13 @@ __global__ __launch_bounds__(BLK) void lazy_ratio_kernel(
 // values of the leaving row.  The window's last slot (q == last) compacts the
 // touched columns into records for the flush, also when the window stopped.
 // ---------------------------------------------------------------------------
-template <int KMAX>
+template <int KMAX, bool FIN = false>
 __global__ __launch_bounds__(BLK) void lazy_norm_kernel(
     const Key* __restrict__ ratio_part, State* st, const Params* __restrict__ prm,
     int n_ratio, int q, const double* __restrict__ A, int64_t ld, int64_t m_local,
     int64_t row0, int64_t N, double* __restrict__ obj, Window win, int last,
-    Key* __restrict__ enter_part, int64_t* __restrict__ basis, int64_t* __restrict__ hist) {
+    Key* __restrict__ enter_part, int64_t* __restrict__ basis, int64_t* __restrict__ hist,
+    const char* __restrict__ gbuf = nullptr, int64_t gstride = 0, int nranks = 0) {
   static_assert(KMAX <= 64, "slots are lane-indexed");
   constexpr int CH = KMAX % 8 == 0 ? 8 : KMAX % 4 == 0 ? 4 : 2;  // slot chunk (divides KMAX)
   const bool block0 = blockIdx.x == 0 && threadIdx.x == 0;
@@ -296,8 +297,18 @@ __global__ __launch_bounds__(BLK) void lazy_norm_kernel(
   const bool live = j < N;
   const int64_t jc = live ? j : 0;
   // --- batch 1 ---
+  // FIN (row-sharded, after the all-gather): the keys are the ranks' payload
+  // headers, lane-indexed; otherwise this GPU's per-wave ratio partials
   Keys8 kk;
-  keys_issue(kk, ratio_part, n_ratio);
+  KeyR gk = keyr_none();
+  if constexpr (FIN) {
+    if (lane < nranks) {
+      const Key* kq = reinterpret_cast<const Key*>(gbuf + lane * gstride);
+      gk = KeyR{kq->v, kq->t, kq->row};
+    }
+  } else {
+    keys_issue(kk, ratio_part, n_ratio);
+  }
   asm volatile("" ::: "memory");  // the keys first (see lazy_ratio)
   double o = obj[jc];
   const uint32_t old = live ? win.tag[jc] : 0u;
@@ -331,8 +342,16 @@ __global__ __launch_bounds__(BLK) void lazy_norm_kernel(
   const int64_t n_enter = prm->n_enter;
   const int64_t iter_limit = prm->iter_limit;
   const bool skip = prm->skip_zero != 0;
-  KeyR rk = keys_reduce(kk, ratio_part, n_ratio);
+  KeyR rk = gk;
+  if constexpr (!FIN) rk = keys_reduce(kk, ratio_part, n_ratio);
   wave_min_dpp(rk);
+  // FIN: the winning rank (t is unique: exactly one header equals the minimum)
+  int wrank = 0;
+  if constexpr (FIN) {
+    const uint64_t hit = __ballot(lane < nranks && gk.row == rk.row && gk.v == rk.v &&
+                                  gk.t == rk.t);
+    wrank = hit ? __builtin_ctzll(hit) : 0;
+  }
   // stop: no pivot in this slot (grid-uniform)
   bool stop = status != ST_RUNNING;
   int32_t new_status = ST_RUNNING;
@@ -349,13 +368,20 @@ __global__ __launch_bounds__(BLK) void lazy_norm_kernel(
   if (block0 && stop) win.made[q] = 0;
   SPX_PROBE(q, 1, 1, !stop);
   // --- batch 2 (row clamped, so the loads are unconditional) ---
-  const int64_t rl = stop ? 0 : r - row0;
-  double v = A[jc * ld + rl];
-  const double piv = win.F[(int64_t)q * ld + rl];
+  // FIN: the winner's normalised row, computed by its owner (lazy_prep_kernel)
+  // with this kernel's own formula
+  const int64_t rl = (stop || FIN) ? 0 : r - row0;
+  double v = 0.0, piv = 1.0, pw = 0.0;
+  if constexpr (FIN) {
+    pw = reinterpret_cast<const double*>(gbuf + wrank * gstride + PAYLOAD_HDR)[jc];
+  } else {
+    v = A[jc * ld + rl];
+    piv = win.F[(int64_t)q * ld + rl];
+  }
   double fr[KMAX];
 #pragma unroll
   for (int c8 = 0; c8 < KMAX; c8 += CH) {
-    if (c8 < q) {
+    if (!FIN && c8 < q) {
 #pragma unroll
       for (int u = 0; u < CH; ++u) fr[c8 + u] = win.F[(int64_t)(c8 + u) * ld + rl];
     } else {
@@ -374,7 +400,7 @@ __global__ __launch_bounds__(BLK) void lazy_norm_kernel(
         const bool act = s < q;
         const bool isr = rl == rdlane64(slot_r, s) - row0;
         const bool isc = jc == rdlane64(slot_c, s);
-        v = apply_sel(v, isr, isc, act, fr[s], ps[s], skip);
+        if constexpr (!FIN) v = apply_sel(v, isr, isc, act, fr[s], ps[s], skip);
         zb |= act && skip && ps[s] == 0.0;
       }
     }
@@ -385,7 +411,7 @@ __global__ __launch_bounds__(BLK) void lazy_norm_kernel(
   if (!stop) {
     KeyR ek = keyr_none();
     if (live) {
-      p = v / piv;
+      p = FIN ? pw : v / piv;
       win.P[j * KW + q] = p;
       const bool nz = (p != 0.0) || !skip;
       if (j == c) {
@@ -450,6 +476,95 @@ __global__ __launch_bounds__(BLK) void lazy_norm_kernel(
     }
   }
   SPX_PROBE(q, 1, 3, true);
+}
+
+// ---------------------------------------------------------------------------
+// lazy_prep_kernel<KMAX> (row-sharded rank, slot q): this rank's leaving-row
+// candidate -- the argmin of its own ratio partials, or the forced row if it
+// owns it -- and that row's CURRENT values (stale row + the pending slots,
+// lazy_norm's formula), normalised, as the all-gather payload [key | p[0..N)].
+// lazy_norm_kernel<KMAX, true> on every rank then takes the lexicographic
+// winner's p: the single-GPU p, bit for bit.  One thread per column.
+// ---------------------------------------------------------------------------
+template <int KMAX>
+__global__ __launch_bounds__(BLK) void lazy_prep_kernel(
+    const Key* __restrict__ ratio_part, const State* st, const Params* __restrict__ prm,
+    int n_ratio, int q, const double* __restrict__ A, int64_t ld, int64_t m_local,
+    int64_t row0, int64_t N, Window win, char* __restrict__ sendbuf, int rank) {
+  static_assert(KMAX <= 64, "slots are lane-indexed");
+  constexpr int CH = KMAX % 8 == 0 ? 8 : KMAX % 4 == 0 ? 4 : 2;
+  const int lane = threadIdx.x & 63;
+  const int64_t j = (int64_t)blockIdx.x * BLK + threadIdx.x;
+  const bool live = j < N;
+  const int64_t jc = live ? j : 0;
+  // --- batch 1 ---
+  Keys8 kk;
+  keys_issue(kk, ratio_part, n_ratio);
+  asm volatile("" ::: "memory");
+  double ps[KMAX];
+  const double* __restrict__ Pj = win.P + jc * KW;
+#pragma unroll
+  for (int c8 = 0; c8 < KMAX; c8 += CH) {
+    if (c8 < q) {
+#pragma unroll
+      for (int u = 0; u < CH; u += 2) {
+        const dbl2 pp = ld2<false>(Pj + c8 + u);
+        ps[c8 + u] = pp.x;
+        ps[c8 + u + 1] = pp.y;
+      }
+    } else {
+#pragma unroll
+      for (int u = 0; u < CH; ++u) ps[c8 + u] = 0.0;
+    }
+  }
+  const int64_t slot_r = win.r[lane < KMAX ? lane : 0];
+  const int64_t slot_c = win.c[lane < KMAX ? lane : 0];
+  const bool go = st->status == ST_RUNNING && st->c_next >= 0;
+  const int64_t forced_r = st->forced_r;
+  const bool skip = prm->skip_zero != 0;
+  KeyR k = keys_reduce(kk, ratio_part, n_ratio);
+  wave_min_dpp(k);
+  if (forced_r >= 0)
+    k = (forced_r >= row0 && forced_r < row0 + m_local) ? KeyR{0.0, 0, forced_r} : keyr_none();
+  const bool have = go && k.row >= 0;  // grid-uniform
+  // --- batch 2 (row clamped) ---
+  const int64_t rl = have ? k.row - row0 : 0;
+  double v = A[jc * ld + rl];
+  const double piv = win.F[(int64_t)q * ld + rl];
+  double fr[KMAX];
+#pragma unroll
+  for (int c8 = 0; c8 < KMAX; c8 += CH) {
+    if (c8 < q) {
+#pragma unroll
+      for (int u = 0; u < CH; ++u) fr[c8 + u] = win.F[(int64_t)(c8 + u) * ld + rl];
+    } else {
+#pragma unroll
+      for (int u = 0; u < CH; ++u) fr[c8 + u] = 0.0;
+    }
+  }
+  asm volatile("" ::: "memory");
+#pragma unroll
+  for (int c8 = 0; c8 < KMAX; c8 += CH) {
+    if (c8 < q) {
+#pragma unroll
+      for (int u = 0; u < CH; ++u) {
+        const int s = c8 + u;
+        const bool act = s < q;
+        const bool isr = rl == rdlane64(slot_r, s) - row0;
+        const bool isc = jc == rdlane64(slot_c, s);
+        v = apply_sel(v, isr, isc, act, fr[s], ps[s], skip);
+      }
+    }
+  }
+  if (have && live) reinterpret_cast<double*>(sendbuf + PAYLOAD_HDR)[j] = v / piv;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    Key o;
+    o.v = have ? k.v : __builtin_inf();
+    o.t = have ? k.t : INT64_MAX;
+    o.row = have ? k.row : -1;
+    o.pad = rank;
+    *reinterpret_cast<Key*>(sendbuf) = o;
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -873,7 +988,7 @@ __global__ __launch_bounds__(BLK) void row_fix_kernel(double* __restrict__ A, in
     return;
 #pragma unroll
   for (int L = 0; L < K; ++L) {
-    if (L >= madeK || !lastL[L]) continue;
+    if (L >= madeK || !lastL[L] || rows[L] < 0 || rows[L] >= m_local) continue;  // not ours
     double x = p[L];
 #pragma unroll
     for (int s = L + 1; s < K; ++s)

@@ -223,7 +223,7 @@ def solve_standard_form(sf: StandardForm, *, device: int = 0, rule: str = "dantz
     (-1: auto_window by size; 0: one pass per pivot)."""
     eng = engine_factory() if engine_factory else DeviceTableau(device)
     if window < 0:
-        window = 0 if getattr(eng, "sharded", False) else auto_window(sf.m, sf.N)
+        window = auto_window(sf.m, sf.N)
     try:
         eng.load(sf.T, sf.basis)
         rec = _Recorder(eng, record, cell_budget)

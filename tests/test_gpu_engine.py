@@ -317,7 +317,7 @@ def test_config3_size_first_pivots_bit_exact(eng_cls):
 
 
 # ----------------------------------------------------------- sharded, nranks > 1
-def _sharded_threads(world, kind, m, n, seed, rule, **solve_kw):
+def _sharded_threads(world, kind, m, n, seed, rule, window=0, **solve_kw):
     from simplex_amd import dist, synth
     uid = bytes([world, m % 251, n % 251, seed % 251]) + os.urandom(124)
     outs, errors = {}, []
@@ -327,6 +327,7 @@ def _sharded_threads(world, kind, m, n, seed, rule, **solve_kw):
             r0, r1 = dist.row_partition(m, world, rank)
             T, obj, basis = synth.tableau_rows(kind, m, n, seed, r0, r1, order="F")
             with dist.ShardedTableau(0, rank, world, uid, local=True) as s:
+                s.set_window(window)
                 s.load_shard(T, obj, basis, m, r0)
                 res = s.solve(rule=rule, **solve_kw)
                 outs[rank] = (r0, r1, res, s.history().tolist(), s.tableau(), s.basis())

@@ -244,12 +244,48 @@ def test_window_sizes_validated(eng_cls):
             e.set_window(good)
 
 
-def test_window_rejected_on_sharded_context():
+@pytest.mark.parametrize("world,kind,m,n,rule,K", [
+    (2, "dense", 200, 300, "dantzig", 8),
+    (3, "dense", 301, 257, "dantzig", 24),
+    (4, "dense", 1024, 2048, "dantzig", 16),
+    (2, "degenerate", 64, 64, "bland", 12),
+    (5, "dense", 7, 9, "dantzig", 4),   # ranks with one or two rows
+])
+def test_window_sharded_virtual_ranks_bit_exact(world, kind, m, n, rule, K):
+    """Row-sharded windows (lazy_prep -> all-gather of [key | current row] ->
+    lazy_norm FINISH per pivot, a local flush per window) through the
+    in-process exchange: every rank's rows, objective row, basis and pivot
+    sequence equal the oracle's full solve."""
+    from simplex_amd import synth
+    from test_gpu_engine import _sharded_threads
+    outs = _sharded_threads(world, kind, m, n, 3, rule, window=K)
+    T, basis = synth.full_tableau(kind, m, n, 3)
+    st, hist = O.solve_tableau(T, basis, rule=rule, max_iters=200000)
+    for rank, (r0, r1, res, h, Tl, b) in outs.items():
+        assert res.status == st
+        assert [tuple(x) for x in h] == hist
+        assert np.array_equal(Tl[:-1], T[r0:r1])
+        assert np.array_equal(Tl[-1], T[-1])
+        assert np.array_equal(b, basis)
+
+
+def test_window_sharded_single_rank_rccl_matches_plain(eng_cls):
+    """A 1-rank RCCL communicator runs the sharded window protocol (prep,
+    ncclAllGather, FINISH) inside the captured window graph: byte-identical
+    to the plain windowed engine."""
     from simplex_amd import dist
+    T, basis = _random_tableau(300, 700, seed=17)
+    with eng_cls(0) as e:
+        e.set_window(16)
+        e.load(T, basis)
+        e.solve(max_iters=70)
+        h0, t0 = e.history().tolist(), e.tableau()
     with dist.ShardedTableau(0, 0, 1, dist.make_unique_id()) as s:
-        with pytest.raises(Exception):
-            s.set_window(8)
-        s.set_window(0)  # off stays allowed
+        s.set_window(16)
+        s.load(T, basis)
+        s.solve(max_iters=70)
+        assert s.history().tolist() == h0
+        assert s.tableau().tobytes() == t0.tobytes()
 
 
 def test_window_config3_size_matches_single_pivot_path(eng_cls):

@@ -16,21 +16,23 @@ from simplex_amd.engine import DeviceTableau  # noqa: E402
 
 m, n, rows = 8192, 8192, int(os.environ.get("SHARD_ROWS", "1024"))
 T, obj, basis = synth.tableau_rows("dense", m, n, 20251205, 0, rows, order="F")
-for mode in ("single", "sharded_rccl1"):
+WINDOWS = [int(x) for x in os.environ.get("SHARD_WINDOWS", "0").split(",")]
+for mode, K in [(m_, k_) for k_ in WINDOWS for m_ in ("single", "sharded_rccl1")]:
     if mode == "single":
         eng = DeviceTableau(0)
     else:
         eng = dist.ShardedTableau(0, 0, 1, dist.make_unique_id())
+    eng.set_window(K)
     # a 1024-row LP on its own: its own basis entries, objective row shared
     eng.load_rows(T, obj, basis[:rows], rows, 0)
     eng.run_pivots(20)
     eng.sync()
-    k = int(os.environ.get("SHARD_PIVOTS", "400"))
+    k = int(os.environ.get("SHARD_PIVOTS", "480"))
     t0 = time.perf_counter()
     eng.run_pivots(k)
     eng.sync()
     el = time.perf_counter() - t0
     st, it, _ = eng.state()
-    print(json.dumps({"mode": mode, "rows": rows, "cols": n + m + 1, "pivots": k,
+    print(json.dumps({"mode": mode, "window": K, "rows": rows, "cols": n + m + 1, "pivots": k,
                       "us_per_pivot": 1e6 * el / k, "status": st, "iters": it}), flush=True)
     eng.close()
