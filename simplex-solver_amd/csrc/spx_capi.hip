@@ -414,7 +414,7 @@ int enqueue_window_t(spx_ctx* ctx, int npiv, bool time_flush) {
   };
   const bool nts = (ctx->elim_nt & 2) != 0;
   // variants: 0 (default) LDS-DMA ring of 12 columns per wave over the
-  // compacted records; 6 / 7 the same with rings of 9 / 16; register rings
+  // compacted records; 6 / 7 the same with rings of 9 / 10; register rings
   // (rows per lane x depth, A = sweep direction alternating per window):
   // 1 2x4, 2 4x4, 3 4x4A, 4 2x8, 5 2x4A (profiles/r01/tune_flush_*.log)
   // (register rings exist for power-of-two windows only; others take the default)
@@ -426,7 +426,7 @@ int enqueue_window_t(spx_ctx* ctx, int npiv, bool time_flush) {
     case 4: if constexpr (POW2) { nts ? go(flush_kernel<KMAX, 2, 8, true>, 2) : go(flush_kernel<KMAX, 2, 8, false>, 2); } break;
     case 5: if constexpr (POW2) { nts ? go(flush_kernel<KMAX, 2, 4, true, true>, 2) : go(flush_kernel<KMAX, 2, 4, false, true>, 2); } break;
     case 6: nts ? go(flush_lds_kernel<KMAX, 9, true>, 2) : go(flush_lds_kernel<KMAX, 9, false>, 2); break;
-    case 7: nts ? go(flush_lds_kernel<KMAX, 16, true>, 2) : go(flush_lds_kernel<KMAX, 16, false>, 2); break;
+    case 7: nts ? go(flush_lds_kernel<KMAX, 10, true>, 2) : go(flush_lds_kernel<KMAX, 10, false>, 2); break;
     default:
       if (npiv < KMAX)  // the last window of a request: every slot guarded
         nts ? go(flush_lds_kernel<KMAX, 12, true, true>, 2) : go(flush_lds_kernel<KMAX, 12, false, true>, 2);
