@@ -149,17 +149,18 @@ int spx_pivot(spx_ctx* ctx, const spx_opts* opts, int64_t* r, int64_t* c);
 int spx_pivot_at(spx_ctx* ctx, int64_t r, int64_t c);
 /* Enqueue exactly `npivots` rule-chosen pivots without host synchronisation
  * (benchmark primitive; pivots after termination are no-ops on the device).
- * If `time_elim` = k > 0, HIP events bracket every k-th elimination launch
- * (event-record nodes inside the replayed hipGraph when use_graph is set). */
+ * If `time_elim` = k > 0, HIP events bracket every k-th elimination launch, or
+ * in window mode every k-th window's flush; the timed launches are direct, the
+ * other windows replay the per-window hipGraph when use_graph is set. */
 int spx_run_pivots(spx_ctx* ctx, const spx_opts* opts, int64_t npivots, int time_elim);
 int spx_sync(spx_ctx* ctx);
 /* Device-side state after spx_sync: status code (SPX_RUNNING while going),
  * total pivots since load, and the objective-row RHS. */
 int spx_state(spx_ctx* ctx, int32_t* status, int64_t* iters, double* objective);
-/* Sum and count of the elimination-kernel event timings collected by
- * spx_run_pivots(..., time_elim=1) since the last reset; `touched_cols`
- * receives the sum over those pivots of the number of columns the kernel
- * updated (for algorithmic-byte accounting). */
+/* Sum and count of the elimination-kernel (or flush) event timings collected
+ * by spx_run_pivots(..., time_elim=k) since the last reset; `touched_cols`
+ * receives the sum, over every pivot (window mode: every flush) since the
+ * reset, of the columns the kernel updated (algorithmic-byte accounting). */
 int spx_elim_timing(spx_ctx* ctx, double* total_ms, int64_t* count, int64_t* touched_cols,
                     int reset);
 
@@ -167,14 +168,16 @@ int spx_elim_timing(spx_ctx* ctx, double* total_ms, int64_t* count, int64_t* tou
  * grid target (0 = auto), non-temporal flags (bit 0 loads, bit 1 stores; -1 = auto) and
  * `interleave`: bit 0 = interleaved column assignment (else contiguous column
  * ranges), bit 1 = disable software pipelining of column pairs, bit 2 = XCD-aware
- * block swizzle. */
+ * block swizzle, bits 8-10 = window flush variant (0 = LDS-DMA ring of 12, the
+ * default; 6 / 7 = rings of 9 / 10; 1-5 = register rings, power-of-two K only). */
 int spx_set_elim_variant(spx_ctx* ctx, int R, int target_wgs, int nt_flags, int interleave);
 /* The elimination variant in use: R, row chunks, column groups, nt flags,
  * interleave, pipelining, leading dimension. */
 int spx_get_elim_variant(const spx_ctx* ctx, int64_t out[7]);
 /* Windowed ("delayed") elimination: apply K pivots per streaming pass over
  * the tableau (K in 2, 4, 8, 12, 16, 24, 32; 0 or 1 = one pass per pivot).
- * Results are bit-identical.  Single-GPU contexts only. */
+ * Results are bit-identical.  Row-sharded contexts run the
+ * same windows with one all-gather per pivot. */
 int spx_set_window(spx_ctx* ctx, int K);
 /* Layout knob: extra doubles of padding per stored column (even, 0..4096);
   * applies to the next spx_load / spx_load_rows; -1 = automatic. */
