@@ -993,7 +993,7 @@ __global__ __launch_bounds__(BLK) void row_fix_kernel(double* __restrict__ A, in
 #pragma unroll
     for (int s = L + 1; s < K; ++s)
       if (s < madeK) x = msub(x, fr[L][s], p[s]);
-    A[j * ld + rows[L]] = x;
+    __builtin_nontemporal_store(x, A + j * ld + rows[L]);  // scattered 8-B writes: no L2 allocate
   }
 }
 
