@@ -25,11 +25,11 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, kind, m, n, seed, rule, q):
+def _worker(rank, world, port, kind, m, n, seed, rule, q, K=0):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        from oracle.sharded_oracle import sharded_solve
+        from oracle.sharded_oracle import sharded_solve, sharded_windowed_solve
         from simplex_amd import dist as sdist, synth
 
         # 1. unique-id exchange (rank 0's id reaches everyone)
@@ -46,23 +46,32 @@ def _worker(rank, world, port, kind, m, n, seed, rule, q):
             dist.all_gather(out, t)
             return [o.numpy() for o in out]
 
-        st, hist = sharded_solve(T, obj, basis, r0, allgather, rule=rule, max_iters=5000)
+        if K:
+            st, hist = sharded_windowed_solve(T, obj, basis, r0, allgather, K=K, rule=rule,
+                                              max_iters=5000)
+        else:
+            st, hist = sharded_solve(T, obj, basis, r0, allgather, rule=rule, max_iters=5000)
         q.put((rank, r0, r1, st, hist, T, obj, basis))
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,kind,m,n,rule", [
-    (2, "dense", 40, 56, "dantzig"),
-    (3, "dense", 31, 45, "dantzig"),
-    (2, "degenerate", 24, 24, "bland"),
+@pytest.mark.parametrize("world,kind,m,n,rule,K", [
+    (2, "dense", 40, 56, "dantzig", 0),
+    (3, "dense", 31, 45, "dantzig", 0),
+    (2, "degenerate", 24, 24, "bland", 0),
+    # the windowed protocol (the bench's N > 1 path): lazy column / row
+    # reconstruction, one all-gather per pivot, a flush every K pivots
+    (2, "dense", 40, 56, "dantzig", 4),
+    (3, "dense", 31, 45, "dantzig", 8),
+    (2, "degenerate", 24, 24, "bland", 8),
 ])
-def test_sharded_protocol_matches_single_process(world, kind, m, n, rule):
+def test_sharded_protocol_matches_single_process(world, kind, m, n, rule, K):
     from simplex_amd import synth
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, kind, m, n, 3, rule, q))
+    procs = [ctx.Process(target=_worker, args=(r, world, port, kind, m, n, 3, rule, q, K))
              for r in range(world)]
     for p in procs:
         p.start()
