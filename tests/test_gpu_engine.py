@@ -515,13 +515,15 @@ def test_sharded_rccl_in_timed_graph(eng_cls):
         assert np.array_equal(s.tableau(), ref)
 
 
-def test_config4_eight_virtual_ranks_full_size(eng_cls):
+@pytest.mark.parametrize("window,k", [(0, 4), (24, 30)])
+def test_config4_eight_virtual_ranks_full_size(eng_cls, window, k):
     """BASELINE config 4: the config-3 tableau (8192 x 16385) row-sharded over
     8 ranks (1024 rows each), here 8 virtual ranks on one GPU exchanging
-    in-process; first pivots bit-exact vs the oracle on every rank."""
+    in-process; first pivots bit-exact vs the oracle on every rank.  window 24:
+    the bench's N > 1 path (a full window and a partial one)."""
     from simplex_amd import dist, synth
     m = n = 8192
-    world, k = 8, 4
+    world = 8
     uid = b"cfg4" + os.urandom(124)
     outs, errors = {}, []
 
@@ -530,6 +532,7 @@ def test_config4_eight_virtual_ranks_full_size(eng_cls):
             r0, r1 = dist.row_partition(m, world, rank)
             Tl, obj, basis = synth.tableau_rows("dense", m, n, 20251205, r0, r1, order="F")
             with dist.ShardedTableau(0, rank, world, uid, local=True) as s:
+                s.set_window(window)
                 s.load_shard(Tl, obj, basis, m, r0)
                 s.solve(max_iters=k)
                 outs[rank] = (r0, r1, s.history().tolist(), s.tableau(), s.basis())
