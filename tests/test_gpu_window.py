@@ -288,14 +288,16 @@ def test_window_sharded_single_rank_rccl_matches_plain(eng_cls):
         assert s.tableau().tobytes() == t0.tobytes()
 
 
-def test_window_config3_size_matches_single_pivot_path(eng_cls):
-    """8192 x 16385 (BASELINE config 3): 48 pivots in 16-windows are
-    byte-identical to 48 single-pivot passes; first 3 vs the oracle."""
+@pytest.mark.parametrize("K", [16, 24])
+def test_window_config3_size_matches_single_pivot_path(eng_cls, K):
+    """8192 x 16385 (BASELINE config 3): 48 pivots in K-windows (K = 24, the
+    bench default: a 3-pivot call, then 45 = one full window and a partial
+    one) are byte-identical to 48 single-pivot passes; first 3 vs the oracle."""
     from simplex_amd import synth
     m = n = 8192
     Tf, obj, basis = synth.tableau_rows("dense", m, n, 20251205, order="F")
     with eng_cls(0) as e:
-        e.set_window(16)
+        e.set_window(K)
         e.load_rows(Tf, obj, basis, m, 0)
         T = np.vstack([np.ascontiguousarray(Tf), obj[None, :]])
         rb = basis.copy()
