@@ -856,12 +856,8 @@ __global__ __launch_bounds__(BLK) void flush_lds_kernel(double* __restrict__ A, 
   typedef const __attribute__((address_space(4))) int64_t ci64;
   cdbl* rec = (cdbl*)win.rec;
   ci64* hdr = (ci64*)win.rec;
-  // (r_s, c_s) of the window's slots, lane-indexed in VGPRs (vector loads, in
-  // the prologue's VMEM batch): the exact path reads them with v_readlane, no
-  // memory round trip per slot
-  static_assert(K <= 64, "slots are lane-indexed");
-  const int64_t slr = win.r[lane < K ? lane : 0];
-  const int64_t slc = win.c[lane < K ? lane : 0];
+  ci64* wr = (ci64*)win.r;
+  ci64* wc = (ci64*)win.c;
   auto rec_of = [&](int k) -> int64_t { return (int64_t)(g + (int64_t)k * G) * RECW; };
   const uint32_t lds0 =
       (uint32_t)(uintptr_t)((__attribute__((address_space(3))) dbl2*)&ring[0]) +
@@ -870,7 +866,6 @@ __global__ __launch_bounds__(BLK) void flush_lds_kernel(double* __restrict__ A, 
   // the DMAs, and a wait it placed inside the loop for f would drain them
 #pragma unroll
   for (int s = 0; s < K; ++s) asm volatile("" ::"v"(f[s][0]), "v"(f[s][1]));
-  asm volatile("" ::"v"(slr), "v"(slc));
   wait_vmcnt<0>();
   // prologue: columns 0..D-1 (a dummy re-read of the last real column past cnt)
   const double* last_src = A + (hdr[rec_of(0)] & 0xffffffffll) * ld + i0c;
@@ -916,13 +911,16 @@ __global__ __launch_bounds__(BLK) void flush_lds_kernel(double* __restrict__ A, 
         }
       }
     } else {
-      // the exact per-element path (columns entered in the window, or with a
-      // zero p_s[j]; ~2K per window): no memory access per slot
+      // (r_s, c_s) reloaded on this rare path: the laundered bases keep the
+      // compiler from hoisting 2K loop-invariant scalars out of the loop
+      ci64* wrk = wr;
+      ci64* wck = wc;
+      asm volatile("" : "+s"(wrk), "+s"(wck));
 #pragma unroll
       for (int s = 0; s < K; ++s) {
         if (s < nm) {
-          const int64_t rl = rdlane64(slr, s) - row0;
-          const int64_t cs = rdlane64(slc, s);
+          const int64_t rl = wrk[s] - row0;
+          const int64_t cs = wck[s];
           x.x = apply_pivot(x.x, i0, j, rl, cs, f[s][0], pv(s), skip);
           x.y = apply_pivot(x.y, i0 + 1, j, rl, cs, f[s][1], pv(s), skip);
         }
