@@ -37,7 +37,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     # defaults: whole windows of the default K (a partial window's flush is a
     # separate, slower code path -- every slot guarded)
-    ap.add_argument("--steps", type=int, default=480)
+    ap.add_argument("--steps", type=int, default=960)
     ap.add_argument("--warmup", type=int, default=48)
     ap.add_argument("--m", type=int, default=8192)
     ap.add_argument("--n", type=int, default=8192)
