@@ -115,6 +115,7 @@ struct spx_ctx {
   int elim_xcd = 0;        // XCD-aware block swizzle
   int flush_bpc[7 * 8] = {};  // resident flush blocks per CU, by (window size, variant); 0 unknown
   int flush_var = 0;       // flush kernel variant (rows per thread x columns per step)
+  int flush_map = 0;       // flush block -> (row chunk, column group) map
   int last_flush_G = 0;    // column groups of the last flush launch
   int n_cu = 0;
   int ld_pad = -1;         // extra doubles per column (-1: auto, 256 for big shards)
@@ -410,7 +411,7 @@ int enqueue_window_t(spx_ctx* ctx, int npiv, bool time_flush) {
     ctx->last_flush_G = G;
     hipLaunchKernelGGL(kern, dim3(rch * G), dim3(BLK), 0, ctx->stream, ctx->A, ctx->ld,
                        ctx->m_local, ctx->row0, ctx->N, ctx->win, npiv, rch, G, ctx->prm,
-                       ctx->st);
+                       ctx->st, ctx->flush_map);
   };
   const bool nts = (ctx->elim_nt & 2) != 0;
   // variants: 0 (default) LDS-DMA ring of 12 columns per wave over the
@@ -419,7 +420,7 @@ int enqueue_window_t(spx_ctx* ctx, int npiv, bool time_flush) {
   // 1 2x4, 2 4x4, 3 4x4A, 4 2x8, 5 2x4A (profiles/r01/tune_flush_*.log)
   // (register rings exist for power-of-two windows only; others take the default)
   constexpr bool POW2 = (KMAX & (KMAX - 1)) == 0;
-  switch (POW2 ? ctx->flush_var : 0) {
+  switch (POW2 || ctx->flush_var >= 6 ? ctx->flush_var : 0) {
     case 1: if constexpr (POW2) { nts ? go(flush_kernel<KMAX, 2, 4, true>, 2) : go(flush_kernel<KMAX, 2, 4, false>, 2); } break;
     case 2: if constexpr (POW2) { nts ? go(flush_kernel<KMAX, 4, 4, true>, 4) : go(flush_kernel<KMAX, 4, 4, false>, 4); } break;
     case 3: if constexpr (POW2) { nts ? go(flush_kernel<KMAX, 4, 4, true, true>, 4) : go(flush_kernel<KMAX, 4, 4, false, true>, 4); } break;
@@ -1157,6 +1158,7 @@ int spx_set_elim_variant(spx_ctx* ctx, int R, int target_wgs, int nt_flags, int 
   ctx->elim_pipe = (interleave & 2) ? 0 : 1;  // bit 1 of `interleave`: disable pipelining
   ctx->elim_xcd = (interleave & 4) ? 1 : 0;   // bit 2: XCD-aware block swizzle
   ctx->flush_var = (interleave >> 8) & 7;     // bits 8-10: windowed flush variant
+  ctx->flush_map = (interleave >> 11) & 3;    // bits 11-12: flush block map
   choose_geometry(ctx);  // also resolves the automatic nt flags
   if (ctx->loaded) {
     if (ctx->rch > ctx->nbr) {  // ratio_part must hold rch partials

@@ -668,7 +668,8 @@ template <int K, int RT, int D, bool NTS, bool ALT = false>
 __global__ __launch_bounds__(BLK) void flush_kernel(double* __restrict__ A, int64_t ld,
                                                     int64_t m_local, int64_t row0, int64_t N,
                                                     Window win, int npiv, int rch, int G,
-                                                    const Params* __restrict__ prm, State* st) {
+                                                    const Params* __restrict__ prm, State* st,
+                                                    int fmap) {
   SPX_PROBE(K, 2, 0, true);
   SPX_PROBE_BLOCK(0);
   int nm = 0;  // pivots made in this window: a prefix of its npiv slots
@@ -676,8 +677,14 @@ __global__ __launch_bounds__(BLK) void flush_kernel(double* __restrict__ A, int6
   if (nm == 0) return;
   const bool full = nm == K;
   const bool skip = prm->skip_zero != 0;
-  const int chunk = blockIdx.x % rch;
-  const int g = blockIdx.x / rch;
+  // block -> (row chunk, column group): group-major (consecutive blocks share
+  // a group), chunk-major with fmap bit 0; bit 1 rotates the group by the chunk
+  int chunk = blockIdx.x % rch, g = blockIdx.x / rch;
+  if (fmap & 1) {
+    g = blockIdx.x % G;
+    chunk = blockIdx.x / G;
+  }
+  if (fmap & 2) g = (g + chunk) % G;
   const int lane = threadIdx.x & 63;
   const int64_t i0 = (int64_t)chunk * BLK * RT + threadIdx.x * (RT == 1 ? 1 : 2);
   constexpr int NP = npairs<RT>();
@@ -816,7 +823,7 @@ __global__ __launch_bounds__(BLK) void flush_lds_kernel(double* __restrict__ A, 
                                                         int64_t N, Window win, int npiv,
                                                         int rch, int G,
                                                         const Params* __restrict__ prm,
-                                                        State* st) {
+                                                        State* st, int fmap) {
   static_assert(D >= 2 && D <= 16, "ring depth");
   __shared__ dbl2 ring[NWAVE * D * 64];
   SPX_PROBE(K, 2, 0, true);
@@ -827,8 +834,14 @@ __global__ __launch_bounds__(BLK) void flush_lds_kernel(double* __restrict__ A, 
   if (nm == 0) return;
   const bool full = nm == K;
   const bool skip = prm->skip_zero != 0;
-  const int chunk = blockIdx.x % rch;
-  const int g = blockIdx.x / rch;
+  // block -> (row chunk, column group): group-major (consecutive blocks share
+  // a group), chunk-major with fmap bit 0; bit 1 rotates the group by the chunk
+  int chunk = blockIdx.x % rch, g = blockIdx.x / rch;
+  if (fmap & 1) {
+    g = blockIdx.x % G;
+    chunk = blockIdx.x / G;
+  }
+  if (fmap & 2) g = (g + chunk) % G;
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform, in an SGPR
   if (chunk == 0 && g == 0 && threadIdx.x == 0) {

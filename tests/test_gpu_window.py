@@ -63,12 +63,13 @@ def _set_flush_variant(e, fv):
     e.set_elim_variant(0, 0, -1, ilv)
 
 
-@pytest.mark.parametrize("fv", range(8))
+@pytest.mark.parametrize("fv", list(range(8)) + [8, 16, 24, 14])
 @pytest.mark.parametrize("K", [2, 12, 16, 24, 32])
 @pytest.mark.parametrize("shape", [(17, 40), (700, 1500), (1537, 2600)])
 def test_window_flush_variants_bit_exact(eng_cls, fv, K, shape):
     """Every flush kernel variant (register rings of 1/2/4 rows per lane, the
-    LDS-DMA ring over compacted records) gives the single-pivot bytes."""
+    LDS-DMA ring over compacted records) and block map (fv >> 3: chunk-major,
+    rotated groups) gives the single-pivot bytes."""
     T, basis = _random_tableau(*shape, seed=shape[0] + 3 * shape[1] + fv)
     with eng_cls(0) as e:
         e.set_window(K)
