@@ -1,9 +1,14 @@
 """Benchmark: pivots/s of the dense fp64 tableau simplex on MI355X.
 
-A "step" is one pivot (entering scan + ratio test + pivot-row normalise +
-Gauss-Jordan elimination of the whole tableau) of BASELINE.json config 3:
-an 8192 x 16384 dense random-feasible LP, tableau 8193 x 16385 fp64 (1.07 GB)
-resident in HBM before timing starts.  With --gpus N > 1 (launched by
+Workload: BASELINE.json config 3, an 8192 x 16384 dense random-feasible LP,
+tableau 8193 x 16385 fp64 (1.07 GB) resident in HBM before timing starts.
+
+A "step" is one streaming pass of the hot path over the tableau: one window of
+K pivots (K = 24 by default: K entering scans + ratio tests + pivot-row
+normalisations, then ONE Gauss-Jordan elimination pass that applies all K
+pivots).  With --window 0 a step is one single-pivot pass.  So
+`--steps 20` times 20 x 24 = 480 pivots; `value` is pivots per second and
+`ms_per_step` the time of one pass (K pivots).  With --gpus N > 1 (launched by
 torch.distributed.run, one process per GPU) the SAME tableau is row-sharded
 across the N GPUs (config 4): strong scaling, value = whole-job pivots/s.
 
@@ -35,10 +40,9 @@ HBM_PEAK_GBPS = 8000.0  # MI355X spec HBM3E peak (MI355X_MICROARCH.md)
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    # defaults: whole windows of the default K (a partial window's flush is a
-    # separate, slower code path -- every slot guarded)
-    ap.add_argument("--steps", type=int, default=960)
-    ap.add_argument("--warmup", type=int, default=48)
+    # steps / warmup count tableau passes: windows of K pivots (1 pivot at --window 0)
+    ap.add_argument("--steps", type=int, default=40)
+    ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--m", type=int, default=8192)
     ap.add_argument("--n", type=int, default=8192)
     ap.add_argument("--seed", type=int, default=20251205)
@@ -50,7 +54,9 @@ def parse():
     ap.add_argument("--R", type=int, default=0, help="elim rows per thread (0: auto)")
     ap.add_argument("--wgs", type=int, default=0, help="elim grid target (0: auto)")
     ap.add_argument("--fv", type=int, default=-1,
-                    help="windowed flush variant 0-7 (0: LDS-DMA ring of 12, the default; see spx_capi.hip)")
+                    help="windowed flush: variant (bits 0-2: 0 LDS-DMA ring of 12, the default; "
+                         "6/7 rings of 9/10; 1-5 register rings, power-of-two K only) + 8 x block "
+                         "map (bits 3-4: 1 chunk-major, 2 groups rotated); -1 default")
     ap.add_argument("--graph", type=int, default=1,
                     help="1: the timed region replays one hipGraph with an event pair "
                          "captured around every elimination; 0: direct launches + events")
@@ -171,24 +177,29 @@ def main():
     eng.load_rows(Tf, obj, basis, m, row0)
     del Tf
     if args.nt >= 0 or args.ilv >= 0 or args.R or args.wgs or args.fv >= 0:
-        v = eng.elim_variant()
-        ilv = ((v["interleave"] | (0 if v["pipeline"] else 2)) if args.ilv < 0 else args.ilv)
-        ilv |= max(args.fv, 0) << 8
-        eng.set_elim_variant(args.R, args.wgs, -1 if args.nt < 0 else args.nt, ilv)
+        fv = max(args.fv, 0)
+        if args.ilv >= 0:
+            eng.set_elim_variant(args.R, args.wgs, -1 if args.nt < 0 else args.nt,
+                                 args.ilv | (fv & 7) << 8 | (fv >> 3 & 3) << 11)
+        else:
+            eng.set_elim_variant(args.R, args.wgs, -1 if args.nt < 0 else args.nt,
+                                 flush_variant=fv & 7, flush_map=fv >> 3 & 3)
     opts = dict(rule=args.rule, skip_zero_cols=not args.dense, use_graph=use_graph, chunk=32)
 
     def barrier():
         if world > 1:
             tdist.barrier()
 
-    eng.run_pivots(args.warmup, **opts)
+    per_step = K if K else 1  # pivots per step (one tableau pass)
+    n_warm, n_timed = args.warmup * per_step, args.steps * per_step
+    eng.run_pivots(n_warm, **opts)
     eng.sync()
     eng.elim_timing(reset=True)
     barrier()
     eng.sync()
     t0 = time.perf_counter()
     every = args.time_every if args.time_every > 0 else (4 if K else 8)
-    eng.run_pivots(args.steps, time_elim=every, **opts)
+    eng.run_pivots(n_timed, time_elim=every, **opts)
     eng.sync()
     t1 = time.perf_counter()
     barrier()
@@ -198,7 +209,7 @@ def main():
         tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
         elapsed = float(t.item())
     status, iters, z = eng.state()
-    if status != 4 or iters != args.warmup + args.steps:
+    if status != 4 or iters != n_warm + n_timed:
         raise SystemExit(f"pivot loop ended early: status {status}, iters {iters}")
     ms_tot, launches, touched = eng.elim_timing(reset=True)
     what = "flush (window pass)" if K else "elimination"
@@ -211,14 +222,14 @@ def main():
     N = n + m + 1
     if K:
         # one flush per window; touched_total counts each flush's column list
-        flushes = -(-args.steps // K)
+        flushes = args.steps
         cols_per_launch = touched / flushes
-        k_eff = args.steps / flushes
+        k_eff = K
         # read+write 16 B per listed element, plus the window's pivot columns
         # f_s (m) and pivot-row values p_s (listed columns)
         alg_bytes = 16.0 * m_local * cols_per_launch + 8.0 * k_eff * (m_local + cols_per_launch)
     else:
-        cols_per_launch = touched / args.steps  # touched_total counts every pivot
+        cols_per_launch = touched / n_timed  # touched_total counts every pivot
         # algorithmic HBM bytes of one elimination launch: read+write 16 B for every
         # touched element except the entering column, which is only written (8 B)
         alg_bytes = 16.0 * m_local * (cols_per_launch - 1.0) + 8.0 * m_local
@@ -237,7 +248,15 @@ def main():
     if hist is not None:
         cpu = cpu_baseline(m, n, args.seed, args.rule, args.cpu_seconds, hist.tolist())
     if rank == 0:
-        value = args.steps / elapsed
+        value = n_timed / elapsed
+        fvar = eng.elim_variant()
+        pow2 = K > 0 and (K & (K - 1)) == 0
+        if not K:
+            kname = "spx::elim_kernel"
+        elif fvar["flush_var"] in (1, 2, 3, 4, 5) and pow2:
+            kname = "spx::flush_kernel"
+        else:
+            kname = "spx::flush_lds_kernel"
         line = {
             "metric": METRIC,
             "value": value,
@@ -246,6 +265,8 @@ def main():
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": 1e3 * elapsed / args.steps,
+            "pivots_per_step": per_step,
+            "pivots_timed": n_timed,
             "higher_is_better": True,
             "scaling": "strong",
             "vs_baseline": None,
@@ -258,14 +279,15 @@ def main():
                        "elimination": "dense sweep" if args.dense else "skip p[j]==0 columns",
                        "timing": ("per-window hipGraph replay" if (use_graph and K)
                                   else "direct launches"),
-                       "elim_variant": eng.elim_variant(),
+                       "elim_variant": fvar,
+                       "step": (f"one tableau pass = a window of {K} pivots" if K
+                                else "one pivot (single-pivot elimination pass)"),
                        "window": K,
                        "parallelism": f"row-shard x{world}" if world > 1 else "single GPU"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBPS,
                          "traffic": traffic,
-                         "kernel": (("spx::flush_lds_kernel" if max(args.fv, 0) in (0, 6, 7)
-                                     else "spx::flush_kernel") if K else "spx::elim_kernel"),
+                         "kernel": kname,
                          "avg_launch_us": avg_ms * 1e3,
                          "alg_bytes_per_launch": alg_bytes,
                          "touched_cols_per_launch": cols_per_launch,

@@ -176,6 +176,10 @@ int spx_set_elim_variant(spx_ctx* ctx, int R, int target_wgs, int nt_flags, int 
 /* The elimination variant in use: R, row chunks, column groups, nt flags,
  * interleave, pipelining, leading dimension. */
 int spx_get_elim_variant(const spx_ctx* ctx, int64_t out[7]);
+/* The window flush in use: variant and block map (bits 8-10 / 11-12 of
+ * spx_set_elim_variant's `interleave`), then the row chunks and column groups
+ * of the last flush launch (0 before the first flush). */
+int spx_get_flush_variant(const spx_ctx* ctx, int64_t out[4]);
 /* Windowed ("delayed") elimination: apply K pivots per streaming pass over
  * the tableau (K in 2, 4, 8, 12, 16, 24, 32; 0 or 1 = one pass per pivot).
  * Results are bit-identical.  Row-sharded contexts run the

@@ -113,10 +113,13 @@ struct spx_ctx {
   int elim_ilv = 1;        // interleaved column assignment
   int elim_pipe = 1;       // software-pipelined column pairs (+12% on config 3)
   int elim_xcd = 0;        // XCD-aware block swizzle
-  int flush_bpc[7 * 8] = {};  // resident flush blocks per CU, by (window size, variant); 0 unknown
+  // resident flush blocks per CU, by kernel instance (every template instance has
+  // its own register / LDS budget, e.g. the guarded partial-window flush)
+  std::map<const void*, int> flush_bpc;
   int flush_var = 0;       // flush kernel variant (rows per thread x columns per step)
   int flush_map = 0;       // flush block -> (row chunk, column group) map
   int last_flush_G = 0;    // column groups of the last flush launch
+  int last_flush_rch = 0;  // row chunks of the last flush launch
   int n_cu = 0;
   int ld_pad = -1;         // extra doubles per column (-1: auto, 256 for big shards)
   int tune_R = 0;          // 0: automatic
@@ -339,19 +342,20 @@ int flush_rch(const spx_ctx* ctx, int rt) {
   return (int)((ctx->m_local + rt * BLK - 1) / (rt * BLK));
 }
 // column groups: fill the resident capacity (blocks/CU x CUs) once, no tail wave
-int flush_groups(spx_ctx* ctx, int slot, const void* kern, int rch) {
+int flush_groups(spx_ctx* ctx, const void* kern, int rch) {
   if (ctx->tune_wgs > 0) return std::max(1, ctx->tune_wgs / rch);
   if (!ctx->n_cu) {
     (void)hipDeviceGetAttribute(&ctx->n_cu, hipDeviceAttributeMultiprocessorCount, ctx->device);
     if (ctx->n_cu <= 0) ctx->n_cu = 256;
   }
-  if (!ctx->flush_bpc[slot]) {
+  int& bpc = ctx->flush_bpc[kern];
+  if (!bpc) {
     int nb = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kern, BLK, 0) != hipSuccess || nb < 1)
       nb = 2;
-    ctx->flush_bpc[slot] = nb;
+    bpc = nb;
   }
-  return std::max(1, ctx->flush_bpc[slot] * ctx->n_cu / rch);
+  return std::max(1, bpc * ctx->n_cu / rch);
 }
 // lazy_ratio grid: one row per thread
 int lazy_ratio_grid(const spx_ctx* ctx) {
@@ -403,12 +407,11 @@ int enqueue_window_t(spx_ctx* ctx, int npiv, bool time_flush) {
     const int rc = record_event(ctx, e->first);
     if (rc) return rc;
   }
-  const int slot = (KMAX == 2 ? 0 : KMAX == 4 ? 1 : KMAX == 8 ? 2 : KMAX == 12 ? 3
-                    : KMAX == 16 ? 4 : KMAX == 24 ? 5 : 6) + 7 * ctx->flush_var;
   auto go = [&](auto kern, int rt) {
     const int rch = flush_rch(ctx, rt);
-    const int G = flush_groups(ctx, slot, (const void*)kern, rch);
+    const int G = flush_groups(ctx, (const void*)kern, rch);
     ctx->last_flush_G = G;
+    ctx->last_flush_rch = rch;
     hipLaunchKernelGGL(kern, dim3(rch * G), dim3(BLK), 0, ctx->stream, ctx->A, ctx->ld,
                        ctx->m_local, ctx->row0, ctx->N, ctx->win, npiv, rch, G, ctx->prm,
                        ctx->st, ctx->flush_map);
@@ -1087,7 +1090,7 @@ int spx_probe_read(unsigned long long* out, int n) {
 }
 // flush grid of the last window (diagnostic)
 int spx_probe_flush_grid(spx_ctx* ctx, int* rch, int* G) {
-  *rch = flush_rch(ctx, ctx->flush_var == 2 || ctx->flush_var == 3 ? 4 : 2);
+  *rch = ctx->last_flush_rch;
   *G = ctx->last_flush_G;
   return 0;
 }
@@ -1213,6 +1216,18 @@ int spx_get_elim_variant(const spx_ctx* ctx, int64_t out[7]) {
   out[4] = ctx->elim_ilv;
   out[5] = ctx->elim_pipe | (ctx->elim_xcd << 1);
   out[6] = ctx->ld;
+  return SPX_OK;
+}
+
+// Window flush in use: variant (bits 8-10 of spx_set_elim_variant's
+// interleave), block map (bits 11-12), and the row chunks / column groups of
+// the last flush launch (0 before the first).
+int spx_get_flush_variant(const spx_ctx* ctx, int64_t out[4]) {
+  if (!ctx || !out) return SPX_E_ARG;
+  out[0] = ctx->flush_var;
+  out[1] = ctx->flush_map;
+  out[2] = ctx->last_flush_rch;
+  out[3] = ctx->last_flush_G;
   return SPX_OK;
 }
 

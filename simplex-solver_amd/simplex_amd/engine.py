@@ -281,11 +281,21 @@ class DeviceTableau:
         return float(ms.value), int(cnt.value), int(cols.value)
 
     def elim_variant(self) -> dict:
+        """The elimination / flush configuration in use.  Keys: R, row_chunks,
+        col_groups, nt_flags, interleave, pipeline (bit 0 software pipelining,
+        bit 1 XCD swizzle), ld, and for the window flush: flush_var, flush_map,
+        flush_row_chunks, flush_groups (the last two from the last flush launch)."""
         out = np.zeros(7, dtype=np.int64)
         self._check(self._lib.spx_get_elim_variant(self._ctx, _lptr(out)),
                     "spx_get_elim_variant")
         keys = ("R", "row_chunks", "col_groups", "nt_flags", "interleave", "pipeline", "ld")
-        return {k: int(v) for k, v in zip(keys, out)}
+        d = {k: int(v) for k, v in zip(keys, out)}
+        fo = np.zeros(4, dtype=np.int64)
+        self._check(self._lib.spx_get_flush_variant(self._ctx, _lptr(fo)),
+                    "spx_get_flush_variant")
+        d.update(flush_var=int(fo[0]), flush_map=int(fo[1]), flush_row_chunks=int(fo[2]),
+                 flush_groups=int(fo[3]))
+        return d
 
     def set_window(self, K: int) -> None:
         """Windowed elimination: K pivots per pass over the tableau (0/1 = off)."""
@@ -296,10 +306,27 @@ class DeviceTableau:
         self._check(self._lib.spx_set_ld_pad(self._ctx, int(pad)), "spx_set_ld_pad")
 
     def set_elim_variant(self, R: int = 0, target_wgs: int = 0, nt_flags: int = -1,
-                         interleave: int = 1) -> None:
-        """Elimination-kernel tuning: rows per thread, grid target, non-temporal
-        flags (1 loads, 2 stores, -1 auto), interleave bits (1 interleaved
-        columns, +2 disables software pipelining)."""
+                         interleave: int = None, *, pipeline: bool = None, xcd: bool = None,
+                         flush_variant: int = None, flush_map: int = None) -> None:
+        """Elimination / flush tuning (spx_set_elim_variant, include/spx.h).
+
+        R: rows per thread (2/4/8, 0 auto); target_wgs: grid target (0 auto);
+        nt_flags: non-temporal bit 0 loads, bit 1 stores (-1 auto).  The C
+        `interleave` word packs: bit 0 interleaved columns, bit 1 pipelining
+        OFF, bit 2 XCD-aware swizzle, bits 8-10 window flush variant (0 the
+        LDS-DMA ring of 12, 6/7 rings of 9/10, 1-5 register rings for
+        power-of-two K), bits 11-12 flush block map (bit 11 chunk-major, bit 12
+        groups rotated by row chunk).  Pass `interleave` to set the whole word,
+        or leave it None and give only the keyword fields to change: the others
+        keep their current values (read back with elim_variant())."""
+        if interleave is None:
+            v = self.elim_variant()
+            pipe = bool(v["pipeline"] & 1) if pipeline is None else bool(pipeline)
+            xc = bool(v["pipeline"] & 2) if xcd is None else bool(xcd)
+            fv = v["flush_var"] if flush_variant is None else int(flush_variant)
+            fm = v["flush_map"] if flush_map is None else int(flush_map)
+            interleave = (v["interleave"] & 1) | (0 if pipe else 2) | (4 if xc else 0)
+            interleave |= (fv & 7) << 8 | (fm & 3) << 11
         self._check(self._lib.spx_set_elim_variant(self._ctx, int(R), int(target_wgs),
                                                    int(nt_flags), int(interleave)),
                     "spx_set_elim_variant")

@@ -58,9 +58,10 @@ def test_window_rule_pivots_bit_exact(eng_cls, K, shape, skip):
 
 
 def _set_flush_variant(e, fv):
+    """fv = flush variant (bits 0-2) + 8 * block map (bits 3-4)."""
+    e.set_elim_variant(0, 0, -1, flush_variant=fv & 7, flush_map=fv >> 3)
     v = e.elim_variant()
-    ilv = (v["interleave"] | (0 if v["pipeline"] else 2)) | (fv << 8)
-    e.set_elim_variant(0, 0, -1, ilv)
+    assert (v["flush_var"], v["flush_map"]) == (fv & 7, fv >> 3)
 
 
 @pytest.mark.parametrize("fv", list(range(8)) + [8, 16, 24, 14])

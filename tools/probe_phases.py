@@ -47,8 +47,7 @@ def main():
     e = DeviceTableau(0)
     e.set_window(K)
     e.load_rows(Tf, obj, basis, a.m, 0)
-    v = e.elim_variant()
-    e.set_elim_variant(0, 0, -1, (v["interleave"] | (0 if v["pipeline"] else 2)) | (a.fv << 8))
+    e.set_elim_variant(0, 0, -1, flush_variant=a.fv & 7, flush_map=a.fv >> 3)
     del Tf
     e.run_pivots(4 * K)
     e.sync()

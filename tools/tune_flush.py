@@ -15,9 +15,11 @@ import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "simplex-solver_amd"))
-if "--probe-lib" in sys.argv:  # diagnostic variants (fv 6, 7) live in the probe build only
+if "--probe-lib" in sys.argv:  # the phase-timing build of tools/probe_phases.py
     os.environ["SPX_LIB"] = os.path.join(ROOT, "simplex-solver_amd", "simplex_amd", "lib",
                                          "libspx_probe.so")
+# (every variant 0-7 is dispatched by the main libspx.so; 1-5 only for
+# power-of-two K, other K fall back to the default LDS-DMA ring)
 
 from simplex_amd import synth  # noqa: E402
 from simplex_amd.engine import DeviceTableau  # noqa: E402
@@ -38,15 +40,13 @@ def main():
     e = DeviceTableau(0)
     e.load_rows(Tf, obj, basis, a.m, 0)
     del Tf
-    v = e.elim_variant()
-    base_ilv = v["interleave"] | (0 if v["pipeline"] else 2)
     e.run_pivots(16)
     e.sync()
     for rnd in range(a.rounds):
         for K in [int(x) for x in a.ks.split(",")]:
             for fv in [int(x) for x in a.fvs.split(",")]:
                 e.set_window(K)
-                e.set_elim_variant(0, a.wgs, -1, base_ilv | (fv << 8))
+                e.set_elim_variant(0, a.wgs, -1, flush_variant=fv & 7, flush_map=fv >> 3)
                 e.run_pivots(2 * K)
                 e.sync()
                 e.elim_timing(reset=True)
