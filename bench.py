@@ -64,6 +64,10 @@ def parse():
     ap.add_argument("--window", type=int, default=-1,
                     help="windowed elimination: K pivots per tableau pass (0 = off, "
                          "-1 = default: %d, on one GPU and on row shards)" % DEFAULT_WINDOW)
+    ap.add_argument("--chain", type=int, default=0,
+                    help="window pivot chain: 0 one persistent launch per window (default, "
+                         "single GPU), 1 two launches per pivot")
+    ap.add_argument("--chain-blocks", type=int, default=0, help="persistent chain grid (0: minimum)")
     ap.add_argument("--time-every", type=int, default=0,
                     help="HIP events around every k-th elimination (or window flush) of the "
                          "timed region (0: 8 eliminations / 4 flushes; an event node costs "
@@ -174,6 +178,8 @@ def main():
     K = 0 if K <= 1 else K
     if K:
         eng.set_window(K)
+    if world == 1:
+        eng.set_chain(args.chain, args.chain_blocks)
     eng.load_rows(Tf, obj, basis, m, row0)
     del Tf
     if args.nt >= 0 or args.ilv >= 0 or args.R or args.wgs or args.fv >= 0:
@@ -283,6 +289,7 @@ def main():
                        "step": (f"one tableau pass = a window of {K} pivots" if K
                                 else "one pivot (single-pivot elimination pass)"),
                        "window": K,
+                       "chain_blocks": eng.chain_blocks() if world == 1 else 0,
                        "parallelism": f"row-shard x{world}" if world > 1 else "single GPU"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBPS,

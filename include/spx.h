@@ -185,6 +185,15 @@ int spx_get_flush_variant(const spx_ctx* ctx, int64_t out[4]);
  * Results are bit-identical.  Row-sharded contexts run the
  * same windows with one all-gather per pivot. */
 int spx_set_window(spx_ctx* ctx, int K);
+/* Pivot chain of a window (the K pivot choices before its flush): mode 0
+ * (default) runs them as ONE persistent launch when the tableau fits (at most
+ * 512 x CUs columns and rows, single-GPU contexts), mode 1 as two
+ * launches per pivot, modes 2 / 3 force the persistent chain's 256- / 512-thread
+ * blocks.  Results are bit-identical.  min_blocks (0..256) raises the
+ * persistent grid above its minimum (tuning; 0 = minimum). */
+int spx_set_chain(spx_ctx* ctx, int mode, int min_blocks);
+/* Blocks of the persistent chain the loaded tableau uses (0: not used). */
+int spx_get_chain(spx_ctx* ctx, int* blocks);
 /* Layout knob: extra doubles of padding per stored column (even, 0..4096);
   * applies to the next spx_load / spx_load_rows; -1 = automatic. */
 int spx_set_ld_pad(spx_ctx* ctx, int pad);

@@ -31,6 +31,7 @@
 #include "../../include/spx.h"
 #include "spx_kernels.hpp"
 #include "spx_delayed.hpp"
+#include "spx_chain.hpp"
 
 using namespace spx;
 
@@ -128,6 +129,13 @@ struct spx_ctx {
   // windowed (delayed) elimination: 0 = off (fused per-pivot elimination)
   int win_k = 0;
   Window win{};
+  // persistent pivot chain of a window (spx_chain.hpp): record buffers and mode
+  unsigned long long* gr_enter = nullptr;  // ENTER_REC x CHAIN_MAX_BLOCKS granules
+  unsigned long long* gr_ratio = nullptr;  // RATIO_REC x CHAIN_MAX_BLOCKS granules
+  unsigned long long* pg = nullptr;        // N x KW x 2 history granules of p_s[j]
+  unsigned long long* fg = nullptr;        // m x KW x 2 history granules of f_s[i]
+  int chain_mode = 0;      // 0: persistent chain when it fits, 1: launch per phase
+  int chain_min_blocks = 0;
 
   // graph cache
   hipGraphExec_t gexec = nullptr;
@@ -201,6 +209,10 @@ int free_buffers(spx_ctx* ctx) {
   dfree(ctx->win.epoch);
   dfree(ctx->win.nlist);
   dfree(ctx->win.rec);
+  dfree(ctx->gr_enter);
+  dfree(ctx->gr_ratio);
+  dfree(ctx->pg);
+  dfree(ctx->fg);
   ctx->loaded = false;
   return SPX_OK;
 }
@@ -332,6 +344,12 @@ int record_event(spx_ctx* ctx, hipEvent_t ev) {
   return SPX_OK;
 }
 
+// entering partial slots: one per wave of the lazy kernels, or one per block of
+// the persistent chain (up to CHAIN_MAX_BLOCKS)
+int enter_part_len(const spx_ctx* ctx) {
+  return std::max(NWAVE * ctx->nbn, CHAIN_MAX_BLOCKS);
+}
+
 // ratio partial slots: prime / fused elim / lazy_ratio grids
 int ratio_part_len(const spx_ctx* ctx) {
   return std::max({ctx->nbr, ctx->rch, NWAVE * (int)((ctx->m_local + BLK - 1) / BLK)});
@@ -362,10 +380,44 @@ int lazy_ratio_grid(const spx_ctx* ctx) {
   return std::max(1, (int)((ctx->m_local + BLK - 1) / BLK));
 }
 
+// Persistent chain geometry: B blocks of CB threads (one per CU, all
+// resident), each owning <= CB columns and <= CB rows.  Returns B (and CB in
+// *cb), or 0 when the chain does not apply (row shards, the launch-per-phase
+// mode, or a tableau wider than CB x CUs columns).  mode 2 / 3 force 256- /
+// 512-thread blocks; automatic: 256 threads (measured faster than 512 at
+// config 3, profiles/r02), 512 when the tableau needs more than 256 blocks.
+int chain_blocks(spx_ctx* ctx, int* cb_out = nullptr) {
+  if (ctx->sharded || ctx->chain_mode == 1) return 0;
+  if (!ctx->n_cu) {
+    (void)hipDeviceGetAttribute(&ctx->n_cu, hipDeviceAttributeMultiprocessorCount, ctx->device);
+    if (ctx->n_cu <= 0) ctx->n_cu = 256;
+  }
+  const int64_t wide = std::max<int64_t>(ctx->N, ctx->m_local);
+  const int cb = ctx->chain_mode == 2 ? 256 : ctx->chain_mode == 3 ? 512
+                 : (wide > 256 * std::min(ctx->n_cu, CHAIN_MAX_BLOCKS) ? 512 : 256);
+  if (cb_out) *cb_out = cb;
+  const int64_t need = std::max<int64_t>({(ctx->N + cb - 1) / cb, (ctx->m_local + cb - 1) / cb,
+                                          1, (int64_t)ctx->chain_min_blocks});
+  const int64_t cap = std::min<int64_t>((int64_t)ctx->n_cu, CHAIN_MAX_BLOCKS);
+  return need <= cap ? (int)need : 0;
+}
+
 template <int KMAX>
 int enqueue_window_t(spx_ctx* ctx, int npiv, bool time_flush) {
   const int nbw = lazy_ratio_grid(ctx);
-  for (int q = 0; q < npiv; ++q) {
+  int cb = BLK;
+  const int B = chain_blocks(ctx, &cb);
+  if (B > 0) {
+    const int cpb = (int)((ctx->N + B - 1) / B);
+    const int rpb = (int)((ctx->m_local + B - 1) / B);
+    auto kern = cb == 512 ? chain_kernel<KMAX, 512> : chain_kernel<KMAX, 256>;
+    hipLaunchKernelGGL(kern, dim3(B), dim3(cb), 0, ctx->stream, ctx->enter_part, ctx->st,
+                       (const Params*)ctx->prm, std::max(NWAVE * ctx->nbn, B),
+                       (const double*)ctx->A, ctx->ld, ctx->m_local, ctx->N, ctx->obj, ctx->win,
+                       npiv, ctx->basis, ctx->hist, ctx->gr_enter, ctx->gr_ratio, ctx->pg,
+                       ctx->fg, cpb, rpb);
+  }
+  for (int q = 0; B == 0 && q < npiv; ++q) {
     hipLaunchKernelGGL(lazy_ratio_kernel<KMAX>, dim3(nbw), dim3(BLK), 0, ctx->stream,
                        (const Key*)ctx->enter_part, ctx->st, (const Params*)ctx->prm,
                        NWAVE * ctx->nbn, q, (const double*)ctx->A, ctx->ld, ctx->m_local,
@@ -552,8 +604,8 @@ int begin_call(spx_ctx* ctx, const spx_opts* o, int64_t fc = -1, int64_t fr = -1
   launch_norm<MODE_INIT>(ctx);
   if (!ctx->win_k) {
     launch_prime(ctx);
-  } else {  // lazy_ratio reduces NWAVE*nbn per-wave partials; INIT wrote the first nbn
-    const int n = (NWAVE - 1) * ctx->nbn;
+  } else {  // the window kernels reduce up to enter_part_len partials; INIT wrote the first nbn
+    const int n = enter_part_len(ctx) - ctx->nbn;
     hipLaunchKernelGGL(fill_none_kernel, dim3((n + BLK - 1) / BLK), dim3(BLK), 0, ctx->stream,
                        ctx->enter_part + ctx->nbn, n);
   }
@@ -593,8 +645,15 @@ int map_status(int32_t st) {
     case ST_OPTIMAL: return SPX_OPTIMAL;
     case ST_UNBOUNDED: return SPX_UNBOUNDED;
     case ST_LIMIT: return SPX_ITER_LIMIT;
+    case ST_FAULT: return SPX_E_STATE;
     default: return SPX_RUNNING;
   }
+}
+
+// The device reported a fault (a persistent-chain exchange timed out).
+int fault(spx_ctx* ctx) {
+  ctx->err = "device fault: a pivot-chain exchange timed out (blocks not co-resident?)";
+  return SPX_E_STATE;
 }
 
 int alloc_common(spx_ctx* ctx, int64_t m_local, int64_t N, int64_t m_global, int64_t row0) {
@@ -615,7 +674,7 @@ int alloc_common(spx_ctx* ctx, int64_t m_local, int64_t N, int64_t m_global, int
   HIPC(hipMalloc(&ctx->list, sizeof(int) * N));
   HIPC(hipMalloc(&ctx->basis, sizeof(int64_t) * std::max<int64_t>(1, m_global)));
   HIPC(hipMalloc(&ctx->hist, sizeof(int64_t) * 2 * ctx->hist_cap));
-  HIPC(hipMalloc(&ctx->enter_part, sizeof(Key) * NWAVE * ctx->nbn));  // per wave (windows)
+  HIPC(hipMalloc(&ctx->enter_part, sizeof(Key) * enter_part_len(ctx)));  // per wave / chain block
   HIPC(hipMalloc(&ctx->ratio_part, sizeof(Key) * ratio_part_len(ctx)));
   {
     HIPC(hipMalloc(&ctx->win.F, sizeof(double) * KW * ctx->ld));
@@ -636,6 +695,18 @@ int alloc_common(spx_ctx* ctx, int64_t m_local, int64_t N, int64_t m_global, int
     HIPC(hipMemsetAsync(ctx->win.c, 0, sizeof(int64_t) * KW, ctx->stream));
     HIPC(hipMemsetAsync(ctx->win.tag, 0, sizeof(uint32_t) * N, ctx->stream));
     HIPC(hipMemsetAsync(ctx->win.epoch, 0, sizeof(uint32_t), ctx->stream));
+    const size_t ge = sizeof(unsigned long long) * ENTER_REC * CHAIN_MAX_BLOCKS;
+    const size_t gq = sizeof(unsigned long long) * RATIO_REC * CHAIN_MAX_BLOCKS;
+    HIPC(hipMalloc(&ctx->gr_enter, ge));
+    HIPC(hipMalloc(&ctx->gr_ratio, gq));
+    HIPC(hipMemsetAsync(ctx->gr_enter, 0, ge, ctx->stream));
+    HIPC(hipMemsetAsync(ctx->gr_ratio, 0, gq, ctx->stream));
+    const size_t gp = sizeof(unsigned long long) * 2 * KW * N;
+    const size_t gf = sizeof(unsigned long long) * 2 * KW * std::max<int64_t>(1, m_local);
+    HIPC(hipMalloc(&ctx->pg, gp));
+    HIPC(hipMalloc(&ctx->fg, gf));
+    HIPC(hipMemsetAsync(ctx->pg, 0, gp, ctx->stream));
+    HIPC(hipMemsetAsync(ctx->fg, 0, gf, ctx->stream));
   }
   if (ctx->sharded) {
     ctx->gstride = round_up(PAYLOAD_HDR + (int64_t)sizeof(double) * N, 256);
@@ -979,6 +1050,7 @@ int spx_solve(spx_ctx* ctx, const spx_opts* opts, spx_result* res) {
     }
   }
   if ((rc = pull_state(ctx))) return rc;  // the final state (after the extra chunk)
+  if (status < 0 || ctx->h_st->status == ST_FAULT) return fault(ctx);
   double z = 0.0;
   HIPC(hipMemcpyAsync(&z, ctx->obj + (ctx->N - 1), sizeof(double), hipMemcpyDeviceToHost,
                       ctx->stream));
@@ -1002,6 +1074,7 @@ int spx_pivot(spx_ctx* ctx, const spx_opts* opts, int64_t* r, int64_t* c) {
   if ((rc = enqueue_pivots(ctx, 1, 0))) return rc;
   if ((rc = pull_state(ctx))) return rc;
   const int status = map_status(ctx->h_st->status);
+  if (status < 0) return fault(ctx);
   if (status == SPX_RUNNING && ctx->h_st->iters == it0 + 1) {
     if (r) *r = ctx->h_st->r;
     if (c) *c = ctx->h_st->c;
@@ -1022,6 +1095,7 @@ int spx_pivot_at(spx_ctx* ctx, int64_t r, int64_t c) {
   // pull the post-pivot state before writing the forced fields back
   if ((rc = pull_state(ctx))) return rc;
   const int32_t st_after = ctx->h_st->status;
+  if (st_after == ST_FAULT) return fault(ctx);
   if ((rc = set_state_fields(ctx, st_after, -1, -1))) return rc;
   if ((rc = pull_state(ctx))) return rc;
   return st_after == ST_RUNNING ? SPX_OK : SPX_E_STATE;
@@ -1088,6 +1162,11 @@ int spx_probe_read(unsigned long long* out, int n) {
                  hipSuccess
              ? 0 : -1;
 }
+int spx_probe_read_chain(unsigned long long* out, int n) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(spx::spx_probe_chain),
+                             sizeof(unsigned long long) * std::min(n, 32 * 4 * 256)) == hipSuccess
+             ? 0 : -1;
+}
 // flush grid of the last window (diagnostic)
 int spx_probe_flush_grid(spx_ctx* ctx, int* rch, int* G) {
   *rch = ctx->last_flush_rch;
@@ -1117,6 +1196,7 @@ int spx_state(spx_ctx* ctx, int32_t* status, int64_t* iters, double* objective) 
   CHECK_ARG(ctx->loaded, "no tableau loaded");
   int rc = pull_state(ctx);
   if (rc) return rc;
+  if (ctx->h_st->status == ST_FAULT) return fault(ctx);
   if (status) *status = map_status(ctx->h_st->status);
   if (iters) *iters = ctx->h_st->iters;
   if (objective) {
@@ -1216,6 +1296,28 @@ int spx_get_elim_variant(const spx_ctx* ctx, int64_t out[7]) {
   out[4] = ctx->elim_ilv;
   out[5] = ctx->elim_pipe | (ctx->elim_xcd << 1);
   out[6] = ctx->ld;
+  return SPX_OK;
+}
+
+// Pivot chain of a window: mode 0 = one persistent launch per window when the
+// tableau fits (<= 512 x CUs columns and rows; single-GPU contexts), 1 = two
+// launches per pivot (lazy_ratio -> lazy_norm), 2 / 3 = the persistent chain
+// with 256- / 512-thread blocks.  min_blocks raises the persistent grid above
+// its minimum (tuning; 0 = minimum).
+int spx_set_chain(spx_ctx* ctx, int mode, int min_blocks) {
+  if (!ctx) return SPX_E_ARG;
+  CHECK_ARG(mode >= 0 && mode <= 3 && min_blocks >= 0 && min_blocks <= CHAIN_MAX_BLOCKS,
+            "chain mode must be 0..3, min_blocks 0..256");
+  ctx->chain_mode = mode;
+  ctx->chain_min_blocks = min_blocks;
+  drop_graphs(ctx);
+  return SPX_OK;
+}
+
+// Blocks of the persistent chain for the loaded tableau (0: not used).
+int spx_get_chain(spx_ctx* ctx, int* blocks) {
+  if (!ctx || !blocks) return SPX_E_ARG;
+  *blocks = ctx->loaded && ctx->win_k ? chain_blocks(ctx) : 0;
   return SPX_OK;
 }
 

@@ -1,0 +1,638 @@
+// spx_chain.hpp — the pivot chain of one window as ONE persistent launch.
+//
+// The windowed path (spx_delayed.hpp) chooses each pivot with two dependent
+// launches, lazy_ratio -> lazy_norm, so every pivot pays two kernel
+// boundaries and two re-reads of partials that another XCD wrote before the
+// boundary (~62 % of a pivot at K = 24).  chain_kernel runs all
+// K pivots of a window in one launch of B co-resident blocks (one per CU) that
+// hand the two all-to-all reductions of a pivot to each other in-launch:
+//
+//   ratio phase q : entering column c_q = winner of the blocks' entering
+//                   records; each block rebuilds column c_q and the RHS on its
+//                   rows (stale + pending slots), stores f_q, and publishes its
+//                   best (ratio, tie, row, pivot element) record;
+//   norm phase q  : leaving row r_q = winner of the ratio records; each block
+//                   rebuilds row r_q on its columns, p_q = row / pivot element,
+//                   updates the objective row and tags, and publishes its best
+//                   entering candidate for pivot q+1.
+//
+// The arithmetic is lazy_ratio's / lazy_norm's, operation for operation (the
+// same apply_sel chain over the pending slots in slot order, the same IEEE
+// divisions), so the window's f_s, p_s, objective row, basis and records are
+// bit-identical to the launch-per-phase chain, and the flush that follows is
+// unchanged.  What changes is only where each value lives between pivots:
+//   * a thread owns one column j and one row i of its block's ranges for the
+//     whole window: p_s[j], f_s[i], the current RHS of row i, basis[i],
+//     obj[j] and tag[j] stay in its registers;
+//   * the only cross-block data are the per-block records (8-byte tagged
+//     granules {tag, 32-bit value}, one sc1 store each: the data is the flag)
+//     and the two history vectors another block needs: P[c][0..q) (the
+//     entering column's p values, owner -> every ratio phase) and F[0..q)[r]
+//     (the leaving row's f values, owner -> every norm phase).  Those are
+//     stored sc1 (write-through) and drained (s_waitcnt vmcnt(0)) by every
+//     storing wave before its block's record is stored, and read with sc1
+//     loads after the record poll matched (MI355X_MICROARCH.md, visibility
+//     table row 1; cdna_hip_programming.md Guideline 16 R1/R2);
+//   * the stale tableau A is not written during the launch: plain loads.
+// Every spin is bounded: a block that waits ~4 s for a record stores
+// ST_FAULT and exits, so the grid always drains (the host reports the fault).
+// Record tags are unique per (window epoch, slot, phase), so records of an
+// earlier window never match; one buffer per phase kind suffices because no
+// block can publish phase q+1's records before every block consumed phase q's.
+#pragma once
+#include "spx_delayed.hpp"
+
+namespace spx {
+
+#ifdef SPX_PHASE_TIMING
+// per-block chain timestamps (tools/probe_phases.py --blocks): [q][event][block],
+// events 0 ratio record stored, 1 ratio poll done, 2 entering record stored,
+// 3 entering poll done (of slot q+1's ratio phase)
+__device__ unsigned long long spx_probe_chain[32 * 4 * 256];
+#define SPX_PROBE_CHAIN(q, ev)                                                            \
+  do {                                                                                   \
+    if (threadIdx.x == 0 && blockIdx.x < 256 && (q) < 32)                                \
+      spx_probe_chain[((q) * 4 + (ev)) * 256 + blockIdx.x] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+#else
+#define SPX_PROBE_CHAIN(q, ev) \
+  do {                         \
+  } while (0)
+#endif
+
+constexpr int32_t ST_FAULT = 5;       // a chain exchange timed out (never on a healthy GPU)
+// Records are stored granule-major: granule g of block b at rec[g * CHAIN_MAX_BLOCKS + b],
+// so one poll instruction of a wave reads 64 blocks' granule g as 512 contiguous bytes.
+// A record is a polled header plus extras that only the winner's record is read for
+// (after the poll, beside the phase's other dependent loads); the extras carry the
+// values computed in the same phase as the record, so no consumer waits on a
+// history granule stored moments before the header.
+constexpr int ENTER_REC = 5;          // o_lo, o_hi, j | extras: p_q[j] lo, hi
+constexpr int ENTER_HDR = 3;
+constexpr int RATIO_REC = 8;          // v_lo, v_hi, row, t (Bland only) | extras: f_q[row] lo, hi,
+constexpr int RATIO_HDR = 4;          //   RHS of row lo, hi
+constexpr int CHAIN_MAX_BLOCKS = 256; // one block per CU
+constexpr unsigned CHAIN_SPIN_MAX = 1u << 22;
+
+typedef __attribute__((address_space(1))) unsigned long long gu64;
+typedef __attribute__((address_space(1))) unsigned gu32;
+
+__device__ __forceinline__ void g_store(gu64* g, unsigned tag, unsigned val) {
+  __hip_atomic_store(g, ((unsigned long long)tag << 32) | val, __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ unsigned long long g_load(const gu64* g) {
+  return __hip_atomic_load(const_cast<gu64*>(g), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// write-through (sc1) store / load of one double
+__device__ __forceinline__ void wt_store(double* p, double v) {
+  __hip_atomic_store((gu64*)p, (unsigned long long)__double_as_longlong(v), __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double wt_load(const double* p) {
+  return __longlong_as_double(
+      (long long)__hip_atomic_load((gu64*)const_cast<double*>(p), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT));
+}
+__device__ __forceinline__ void drain_stores() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+// granule kinds
+constexpr int GK_RATIO = 0;  // ratio record of slot q
+constexpr int GK_ENTER = 1;  // entering record published by slot q (for slot q+1)
+constexpr int GK_PHIST = 2;  // p_q[j] of a column (history granules)
+constexpr int GK_FHIST = 3;  // f_q[i] of a row (history granules)
+// granule tag: never 0 (the buffers start zeroed), unique per (epoch, slot, kind)
+__device__ __forceinline__ unsigned rec_tag(uint32_t epoch, int q, int kind) {
+  return 0x80000000u | ((epoch & 0x7fffffu) << 8) | ((unsigned)q << 2) | (unsigned)kind;
+}
+// a double as two granules (low word, high word) at g[0], g[stride]
+__device__ __forceinline__ void g_store_d(gu64* g, unsigned tag, double v, int stride = 1) {
+  const unsigned long long x = (unsigned long long)__double_as_longlong(v);
+  g_store(g, tag, (unsigned)x);
+  g_store(g + stride, tag, (unsigned)(x >> 32));
+}
+__device__ __forceinline__ double g_decode_d(unsigned long long lo, unsigned long long hi) {
+  return __longlong_as_double((long long)((lo & 0xffffffffull) | (hi << 32)));
+}
+
+// argmin key + two doubles of payload, lexicographic on (v, t) as kmin
+struct KeyP {
+  double v;
+  int64_t t;
+  int64_t row;
+  double a, b;
+};
+__device__ __forceinline__ KeyP keyp_none() {
+  return KeyP{__builtin_inf(), INT64_MAX, -1, 0.0, 0.0};
+}
+__device__ __forceinline__ void kmin2(KeyP& k, double v, int64_t t, int64_t row, double a,
+                                      double b) {
+  const bool take = (v < k.v) || (v == k.v && t < k.t);
+  k.v = take ? v : k.v;
+  k.t = take ? t : k.t;
+  k.row = take ? row : k.row;
+  k.a = take ? a : k.a;
+  k.b = take ? b : k.b;
+}
+__device__ __forceinline__ double dbits(int64_t x) { return __longlong_as_double(x); }
+__device__ __forceinline__ int64_t ibits(double x) { return __double_as_longlong(x); }
+template <int CTRL>
+__device__ __forceinline__ void kmin2_dpp(KeyP& k) {
+  kmin2(k, dbits(dpp64<CTRL>(ibits(k.v))), dpp64<CTRL>(k.t), dpp64<CTRL>(k.row),
+        dbits(dpp64<CTRL>(ibits(k.a))), dbits(dpp64<CTRL>(ibits(k.b))));
+}
+template <int D>
+__device__ __forceinline__ void kmin2_swap(KeyP& k) {
+  kmin2(k, dbits(swap64<D>(ibits(k.v))), swap64<D>(k.t), swap64<D>(k.row),
+        dbits(swap64<D>(ibits(k.a))), dbits(swap64<D>(ibits(k.b))));
+}
+// every lane receives the wave's winner and its payload
+__device__ __forceinline__ void wave_min2(KeyP& k) {
+  kmin2_dpp<0x128>(k);  // row_ror:8
+  kmin2_dpp<0x124>(k);  // row_ror:4
+  kmin2_dpp<0x4E>(k);   // quad_perm [2,3,0,1]
+  kmin2_dpp<0xB1>(k);   // quad_perm [1,0,3,2]
+  kmin2_swap<16>(k);
+  kmin2_swap<32>(k);
+}
+// Block argmin (+ payload) of NW waves into thread 0.  All threads must call it.
+template <int NW>
+__device__ __forceinline__ void block_min2(KeyP& k) {
+  __shared__ KeyP sk[NW];
+  wave_min2(k);
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) sk[w] = k;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+#pragma unroll
+    for (int x = 1; x < NW; ++x) kmin2(k, sk[x].v, sk[x].t, sk[x].row, sk[x].a, sk[x].b);
+  }
+}
+
+// Bounded spin bookkeeping: true (and ST_FAULT stored) once a wait ran too long.
+__device__ __forceinline__ bool spin_fail(unsigned& spins, State* st) {
+  if (++spins < CHAIN_SPIN_MAX) {
+    __builtin_amdgcn_s_sleep(1);
+    return false;
+  }
+  if ((threadIdx.x & 63) == 0)
+    __hip_atomic_store((gu32*)&st->status, (unsigned)ST_FAULT, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+  return true;
+}
+
+// Poll the B record headers of one phase (lane l reads blocks l, l+64, ...)
+// until every tag matches; reduce the keys over the wave.  The key's payload
+// `a` is the entering record's objective entry (z_c); `b` the winning block.
+// Returns false on timeout (ST_FAULT stored).  RATIO selects the record kind,
+// G the header granules read (3, or 4 for Bland's ratio records).
+template <bool RATIO>
+__device__ __forceinline__ void decode_record(KeyP& k, const unsigned long long (&g)[4], int b,
+                                              int rule) {
+  const double v = g_decode_d(g[0], g[1]);
+  const unsigned idx = (unsigned)g[2];
+  if (idx == 0xffffffffu) return;
+  if constexpr (RATIO) {
+    // Dantzig ties go to the lowest row (t = row); Bland's to the lowest
+    // basic-variable index (granule 3)
+    kmin2(k, v, rule == RULE_BLAND ? (int64_t)(unsigned)g[3] : (int64_t)idx, (int64_t)idx, 0.0,
+          (double)b);
+  } else {
+    // Dantzig: most negative reduced cost; Bland: lowest index (key 0)
+    kmin2(k, rule == RULE_BLAND ? 0.0 : v, (int64_t)idx, (int64_t)idx, v, (double)b);
+  }
+}
+
+template <bool RATIO, int G>
+__device__ __forceinline__ bool poll_records(const gu64* recs, int B, unsigned tag, int rule,
+                                             KeyP& k, State* st) {
+  const int lane = threadIdx.x & 63;
+  const unsigned long long none = (unsigned long long)tag << 32;
+  if (B <= 64) {
+    // one record per lane: three passes in flight, staggered, so a record is
+    // seen about one load latency after it lands instead of up to two
+    const bool live = lane < B;
+    const gu64* r = recs + (live ? lane : 0);  // (idle lanes re-read block 0: no branch)
+    unsigned long long x0[4], x1[4], x2[4];
+    auto issue = [&](unsigned long long (&g)[4]) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) g[u] = u < G ? g_load(r + (size_t)u * CHAIN_MAX_BLOCKS) : none;
+    };
+    auto good = [&](const unsigned long long (&g)[4]) {
+      bool ok = true;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) ok &= (unsigned)(g[u] >> 32) == tag;
+      return __all(ok);
+    };
+    issue(x0);
+    __builtin_amdgcn_s_sleep(8);
+    issue(x1);
+    __builtin_amdgcn_s_sleep(8);
+    issue(x2);
+    int hit;
+    for (unsigned spins = 0;; ++spins) {
+      if (good(x0)) { hit = 0; break; }
+      issue(x0);
+      if (good(x1)) { hit = 1; break; }
+      issue(x1);
+      if (good(x2)) { hit = 2; break; }
+      issue(x2);
+      if (spins >= CHAIN_SPIN_MAX / 4) {
+        if (lane == 0)
+          __hip_atomic_store((gu32*)&st->status, (unsigned)ST_FAULT, __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+        return false;
+      }
+    }
+    k = keyp_none();
+    unsigned long long g[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) g[u] = hit == 0 ? x0[u] : hit == 1 ? x1[u] : x2[u];
+    if (live) decode_record<RATIO>(k, g, lane, rule);
+  } else {
+    for (unsigned spins = 0;;) {
+      bool ok = true;
+      k = keyp_none();
+      for (int b = lane; b < B; b += 64) {
+        unsigned long long g[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) g[u] = u < G ? g_load(recs + (size_t)u * CHAIN_MAX_BLOCKS + b) : none;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) ok &= (unsigned)(g[u] >> 32) == tag;
+        decode_record<RATIO>(k, g, b, rule);
+      }
+      if (__all(ok)) break;
+      if (spin_fail(spins, st)) return false;
+    }
+  }
+  wave_min2(k);
+  asm volatile("" ::: "memory");  // the loads that follow must not be hoisted above the poll
+  return true;
+}
+
+// The dependent loads of a phase: lane s < n reads history slot s of one
+// column / row (granules h[2s], h[2s+1], tag of slot s), and every lane reads
+// NE doubles of extras (granule pairs at e + 2x*CHAIN_MAX_BLOCKS, tag etag).
+// One pass re-reads until every granule matches.  Returns false on timeout.
+template <int NE>
+__device__ __forceinline__ bool load_phase(const gu64* h, int n, uint32_t W, int kind,
+                                           const gu64* e, unsigned etag, double& hv,
+                                           double (&ev)[2], State* st) {
+  const int lane = threadIdx.x & 63;
+  const bool mine = lane < n;
+  const unsigned tag = rec_tag(W, lane, kind);
+  const gu64* g = h + 2 * (mine ? lane : 0);
+  for (unsigned spins = 0;;) {
+    unsigned long long lo = 0, hi = 0, x[2 * NE > 0 ? 2 * NE : 1];
+    if (mine) {
+      lo = g_load(g);
+      hi = g_load(g + 1);
+    }
+#pragma unroll
+    for (int u = 0; u < 2 * NE; ++u) x[u] = g_load(e + (size_t)u * CHAIN_MAX_BLOCKS);
+    bool good = !mine || ((unsigned)(lo >> 32) == tag && (unsigned)(hi >> 32) == tag);
+#pragma unroll
+    for (int u = 0; u < 2 * NE; ++u) good &= (unsigned)(x[u] >> 32) == etag;
+    if (__all(good)) {
+      hv = mine ? g_decode_d(lo, hi) : 0.0;
+#pragma unroll
+      for (int u = 0; u < NE; ++u) ev[u] = g_decode_d(x[2 * u], x[2 * u + 1]);
+      return true;
+    }
+    if (spin_fail(spins, st)) return false;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// chain_kernel<KMAX, CB>: the pivots of one window (npiv <= KMAX slots),
+// single GPU (row0 = 0).  grid = B blocks of CB threads (one block per CU,
+// every block resident); block b owns columns [b*cpb, ...) and rows
+// [b*rpb, ...), cpb, rpb <= CB, one of each per thread.  Wave 0 of a block
+// polls the record headers and hands the winner to the block through LDS;
+// every thread then loads what its column / row needs.  n_ep / enter_part:
+// pivot 0's entering partials, written by the previous kernel (norm<INIT> or
+// the previous window's chain); the chain writes one partial per block there
+// for the next window.  pg / fg: history granules of every column / row (2 per
+// slot), read by later phases (the newest slot travels in the records).
+// ---------------------------------------------------------------------------
+template <int KMAX, int CB>
+__global__ __launch_bounds__(CB) void chain_kernel(
+    Key* __restrict__ enter_part, State* st, const Params* __restrict__ prm, int n_ep,
+    const double* __restrict__ A, int64_t ld, int64_t m, int64_t N, double* __restrict__ obj,
+    Window win, int npiv, int64_t* __restrict__ basis, int64_t* __restrict__ hist,
+    unsigned long long* gr_enter_, unsigned long long* gr_ratio_, unsigned long long* pg_,
+    unsigned long long* fg_, int cpb, int rpb) {
+  static_assert(KMAX <= 32, "slots are lane-indexed and fit the window buffers");
+  constexpr int NW = CB / 64;
+  constexpr int CH = KMAX % 8 == 0 ? 8 : KMAX % 4 == 0 ? 4 : 2;
+  // one block per CU: the record protocol is validated for that residency
+  __shared__ double lds_pin[88 * 128];
+  __shared__ int64_t bc_idx;  // the winner handed from wave 0 to the block
+  __shared__ double bc_val;
+  __shared__ int bc_blk;
+  gu64* gr_enter = (gu64*)gr_enter_;
+  gu64* gr_ratio = (gu64*)gr_ratio_;
+  gu64* pg = (gu64*)pg_;
+  gu64* fg = (gu64*)fg_;
+  const int B = gridDim.x;
+  const int b = blockIdx.x;
+  const int t = threadIdx.x;
+  const int lane = t & 63;
+  const bool w0 = t < 64;
+  const bool leader = b == 0 && t == 0;
+  // --- everything that does not depend on a pivot, in one batch ---
+  const int32_t status0 = st->status;
+  const int64_t forced_c = st->forced_c;
+  const int64_t forced_r = st->forced_r;
+  const int64_t it0 = st->iters;
+  const int64_t hist_cap = st->hist_cap;
+  const uint32_t E = *win.epoch;
+  const int32_t rule = prm->rule;
+  const double eps_piv = prm->eps_piv;
+  const double eps_opt = prm->eps_opt;
+  const int64_t n_enter = prm->n_enter;
+  const int64_t iter_limit = prm->iter_limit;
+  const bool skip = prm->skip_zero != 0;
+  const uint32_t W = (E + 1u) & TAG_EPOCH;  // this window's epoch
+  // my column and my row
+  const int64_t j = (int64_t)b * cpb + t;
+  const bool jlive = t < cpb && j < N;
+  const int64_t jc = jlive ? j : 0;
+  const int64_t i = (int64_t)b * rpb + t;
+  const bool ilive = t < rpb && i < m;
+  const int64_t ic = ilive ? i : 0;
+  double o = obj[jc];
+  uint32_t tg = jlive ? win.tag[jc] : 0u;
+  const uint32_t tg0 = tg;
+  double bcur = A[(N - 1) * ld + ic];   // current RHS of my row (stale + applied slots)
+  int64_t bas = basis[ic];              // basis[i] (Bland's tie key)
+  double fs[KMAX], ps[KMAX];            // f_s[i], p_s[j] of this window
+#pragma unroll
+  for (int s = 0; s < KMAX; ++s) fs[s] = ps[s] = 0.0;
+  int64_t slot_r = 0, slot_c = -1;      // lane s: (r_s, c_s)
+  if (t == 0) lds_pin[b & 127] = 0.0;
+  if (status0 != ST_RUNNING) {          // grid-uniform: no pivot in this window
+    if (leader)
+      for (int s = 0; s < npiv; ++s) win.made[s] = 0;  // (the flush counts made slots)
+    return;
+  }
+  if (leader) {
+    // the flush's record counter; reset write-through and drained before this
+    // block's first record (every other block adds to it only after polling
+    // that record)
+    __hip_atomic_store((gu32*)win.nlist, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  int q = 0;
+  int64_t r_prev = -1;
+  double f_prev = 0.0, prhs = 0.0;  // my f_{q-1}[i]; p_{q-1}[rhs] = RHS of r_{q-1} / pivot
+  int32_t stop_status = ST_RUNNING;
+  for (; q < npiv; ++q) {
+    // ================= ratio phase q =================
+    SPX_PROBE(q, 0, 0, true);
+    int64_t c;
+    double zc;
+    int wb = 0;
+    if (q == 0) {
+      // entering partials of the previous kernel (visible: kernel boundary)
+      Keys8 kk;
+      keys_issue(kk, enter_part, n_ep);
+      KeyR e = keys_reduce(kk, enter_part, n_ep);
+      wave_min_dpp(e);
+      c = e.row;
+      zc = c >= 0 ? obj[c] : 0.0;
+    } else {
+      if (w0) {
+        KeyP e;
+        const bool ok =
+            poll_records<false, 3>(gr_enter, B, rec_tag(W, q - 1, GK_ENTER), rule, e, st);
+        if (t == 0) {
+          bc_idx = ok ? e.row : -2;
+          bc_val = e.a;
+          bc_blk = (int)e.b;
+        }
+        SPX_PROBE_CHAIN(q - 1, 3);
+      }
+      __syncthreads();
+      c = bc_idx;
+      zc = bc_val;
+      wb = bc_blk;
+      if (c == -2) return;  // a wait timed out (ST_FAULT stored)
+    }
+    SPX_PROBE(q, 0, 1, true);
+    if (forced_c >= 0) {
+      c = forced_c;
+      zc = obj[c];  // (forced pivots are single-pivot windows: q == 0)
+    }
+    const int64_t it = it0 + q;
+    if (c < 0) stop_status = ST_OPTIMAL;
+    else if (forced_r < 0 && it >= iter_limit) stop_status = ST_LIMIT;
+    if (stop_status != ST_RUNNING) break;  // grid-uniform
+    // column c and the RHS on my row: stale + pending slots, in slot order.
+    // p_s[c]: slots < q-1 from the history granules (lane s), slot q-1 from the
+    // winning entering record's extras
+    double fv = A[c * ld + ic];
+    double pcl = 0.0, pnew[2] = {0.0, 0.0};
+    if (q > 0 &&
+        !load_phase<1>(pg + (size_t)c * 2 * KW, q - 1, W, GK_PHIST,
+                       gr_enter + ENTER_HDR * CHAIN_MAX_BLOCKS + wb, rec_tag(W, q - 1, GK_ENTER),
+                       pcl, pnew, st))
+      return;
+    // RHS: apply slot q-1 (the slots before it are already in bcur)
+    if (q > 0) bcur = apply_sel(bcur, i == r_prev, false, true, f_prev, prhs, skip);
+#pragma unroll
+    for (int c8 = 0; c8 < KMAX; c8 += CH) {
+      if (c8 < q) {
+#pragma unroll
+        for (int u = 0; u < CH; ++u) {
+          const int s = c8 + u;
+          const bool act = s < q;
+          const bool isr = i == rdlane64(slot_r, s);
+          const bool isc = c == rdlane64(slot_c, s);
+          const double p_s = (s == q - 1) ? pnew[0] : rdlane(pcl, s);
+          fv = apply_sel(fv, isr, isc, act, fs[s], p_s, skip);
+        }
+      }
+    }
+#pragma unroll
+    for (int s = 0; s < KMAX; ++s) fs[s] = (s == q) ? fv : fs[s];
+    f_prev = fv;
+    KeyP k = keyp_none();
+    if (ilive) {
+      win.F[(int64_t)q * ld + i] = fv;  // for the flush / row_fix (later kernels)
+      g_store_d(fg + (size_t)i * 2 * KW + 2 * q, rec_tag(W, q, GK_FHIST), fv);
+      if (forced_r >= 0) {
+        if (i == forced_r) kmin2(k, 0.0, 0, i, fv, bcur);
+      } else if (fv > eps_piv) {
+        const double rq = bcur / fv;
+        if (rq == rq) kmin2(k, rq, rule == RULE_BLAND ? bas : i, i, fv, bcur);
+      }
+    }
+    SPX_PROBE(q, 0, 2, fv != 12345.678);
+    block_min2<NW>(k);
+    if (t == 0) {
+      gu64* rr = gr_ratio + b;
+      const unsigned tag = rec_tag(W, q, GK_RATIO);
+      const bool none = k.row < 0;
+      // extras first: f_q[row] (the pivot element) and the row's current RHS
+      g_store_d(rr + 4 * CHAIN_MAX_BLOCKS, tag, k.a, CHAIN_MAX_BLOCKS);
+      g_store_d(rr + 6 * CHAIN_MAX_BLOCKS, tag, k.b, CHAIN_MAX_BLOCKS);
+      const unsigned long long vb = (unsigned long long)__double_as_longlong(k.v);
+      g_store(rr + 0 * CHAIN_MAX_BLOCKS, tag, (unsigned)vb);
+      g_store(rr + 1 * CHAIN_MAX_BLOCKS, tag, (unsigned)(vb >> 32));
+      g_store(rr + 2 * CHAIN_MAX_BLOCKS, tag, none ? 0xffffffffu : (unsigned)k.row);
+      g_store(rr + 3 * CHAIN_MAX_BLOCKS, tag, none ? 0xffffffffu : (unsigned)k.t);
+    }
+    SPX_PROBE_CHAIN(q, 0);
+    SPX_PROBE(q, 0, 3, true);
+    // ================= norm phase q =================
+    SPX_PROBE(q, 1, 0, true);
+    if (w0) {
+      KeyP rk;
+      const unsigned rtag = rec_tag(W, q, GK_RATIO);
+      const bool ok = rule == RULE_BLAND
+                          ? poll_records<true, 4>(gr_ratio, B, rtag, rule, rk, st)
+                          : poll_records<true, 3>(gr_ratio, B, rtag, rule, rk, st);
+      if (t == 0) {
+        bc_idx = ok ? rk.row : -2;
+        bc_blk = (int)rk.b;
+      }
+      SPX_PROBE_CHAIN(q, 1);
+    }
+    __syncthreads();
+    const int64_t r = bc_idx;
+    wb = bc_blk;
+    if (r == -2) return;
+    SPX_PROBE(q, 1, 1, true);
+    if (q == 0 && leader) *win.epoch = W;  // every block has read E (its record carries W)
+    if (r < 0) {
+      stop_status = ST_UNBOUNDED;
+      break;
+    }
+    // row r on my column: stale + pending slots.  f_s[r] for s < q from the
+    // history granules (lane s); the pivot element f_q[r] and the row's RHS
+    // from the winning ratio record's extras
+    double v = A[jc * ld + r];
+    double frl = 0.0, ex[2];
+    if (!load_phase<2>(fg + (size_t)r * 2 * KW, q, W, GK_FHIST,
+                       gr_ratio + 4 * CHAIN_MAX_BLOCKS + wb, rec_tag(W, q, GK_RATIO), frl, ex, st))
+      return;
+    const double piv = ex[0];
+    prhs = ex[1] / piv;  // p_q[rhs]: lazy_norm's p = v / piv of the RHS column
+    bool zb = false;
+#pragma unroll
+    for (int c8 = 0; c8 < KMAX; c8 += CH) {
+      if (c8 < q) {
+#pragma unroll
+        for (int u = 0; u < CH; ++u) {
+          const int s = c8 + u;
+          const bool act = s < q;
+          const bool isr = r == rdlane64(slot_r, s);
+          const bool isc = jc == rdlane64(slot_c, s);
+          v = apply_sel(v, isr, isc, act, rdlane(frl, s), ps[s], skip);
+          zb |= act && skip && ps[s] == 0.0;
+        }
+      }
+    }
+    KeyP ek = keyp_none();
+    if (jlive) {
+      const double p = v / piv;
+#pragma unroll
+      for (int s = 0; s < KMAX; ++s) ps[s] = (s == q) ? p : ps[s];
+      win.P[j * KW + q] = p;  // for row_fix (a later kernel)
+      g_store_d(pg + (size_t)j * 2 * KW + 2 * q, rec_tag(W, q, GK_PHIST), p);
+      const bool nz = (p != 0.0) || !skip;
+      if (j == c) {
+        o = 0.0;
+      } else if (nz) {
+        o = msub(o, zc, p);
+      }
+      const bool tagged = (tg & TAG_EPOCH) == W;
+      if (nz) {
+        tg = W | ((j == c || (tagged && (tg & TAG_SPECIAL))) ? TAG_SPECIAL : 0u) |
+             (zb ? TAG_ZERO : 0u);
+      } else if (tagged) {
+        tg = tg | TAG_ZERO;
+      }
+      // key (o, j) under Dantzig, (0, j) under Bland; payload o (z_c) and p_q[j]
+      if (j < n_enter && o < -eps_opt) kmin2(ek, rule == RULE_BLAND ? 0.0 : o, j, j, o, p);
+    }
+    if (ilive && i == r) bas = c;
+    if (lane == q) {
+      slot_r = r;
+      slot_c = c;
+    }
+    r_prev = r;
+    if (leader) {
+      st->r = r;
+      st->c = c;
+      st->zc = zc;
+      st->piv = piv;
+      win.r[q] = r;
+      win.c[q] = c;
+      win.made[q] = 1;
+      basis[r] = c;
+      if (it < hist_cap) {
+        hist[2 * it] = r;
+        hist[2 * it + 1] = c;
+      }
+    }
+    SPX_PROBE(q, 1, 2, v != 12345.678);
+    block_min2<NW>(ek);
+    if (t == 0) {
+      if (q + 1 < npiv) {
+        gu64* er = gr_enter + b;
+        const unsigned tag = rec_tag(W, q, GK_ENTER);
+        g_store_d(er + ENTER_HDR * CHAIN_MAX_BLOCKS, tag, ek.b, CHAIN_MAX_BLOCKS);  // extras: p_q[j]
+        const unsigned long long ob = (unsigned long long)__double_as_longlong(ek.a);
+        g_store(er + 0 * CHAIN_MAX_BLOCKS, tag, (unsigned)ob);
+        g_store(er + 1 * CHAIN_MAX_BLOCKS, tag, (unsigned)(ob >> 32));
+        g_store(er + 2 * CHAIN_MAX_BLOCKS, tag, ek.row < 0 ? 0xffffffffu : (unsigned)ek.row);
+      } else {
+        // the next window's pivot-0 partial (read after the kernel boundary)
+        store_key(enter_part + b, KeyR{ek.v, ek.t, ek.row});
+      }
+      SPX_PROBE_CHAIN(q, 2);
+    }
+    SPX_PROBE(q, 1, 3, true);
+  }
+  // ---- the window ends after slot q (q pivots made) ----
+  if (stop_status != ST_RUNNING && leader) {
+    st->status = stop_status;
+    if (stop_status == ST_OPTIMAL) st->c_next = -1;
+    for (int s = q; s < npiv; ++s) win.made[s] = 0;
+  }
+  if (jlive) {
+    obj[j] = o;
+    if (tg != tg0) win.tag[j] = tg;
+  }
+  if (q == 0) return;  // no pivot made: nothing to compact (the flush sees nm == 0)
+  // compact the window's touched columns into records for the flush (as
+  // lazy_norm's last slot): wave ballot + LDS prefix + one atomic per block
+  const bool mine = jlive && (tg & TAG_EPOCH) == W;
+  __shared__ int wcnt[NW];
+  __shared__ int base;
+  const uint64_t bal = __ballot(mine);
+  const int w = t >> 6;
+  if (lane == 0) wcnt[w] = __popcll(bal);
+  __syncthreads();
+  if (t == 0) {
+    int tot = 0;
+    for (int x = 0; x < NW; ++x) tot += wcnt[x];
+    base = tot ? (int)__hip_atomic_fetch_add((gu32*)win.nlist, (unsigned)tot, __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT)
+               : 0;
+  }
+  __syncthreads();
+  int pos = base + __popcll(bal & ((1ull << lane) - 1ull));
+  for (int x = 0; x < w; ++x) pos += wcnt[x];
+  if (mine && pos < N) {
+    double* rc_ = win.rec + (int64_t)pos * RECW;
+    reinterpret_cast<int64_t*>(rc_)[0] = j | ((int64_t)(tg >> 30) << 32);
+#pragma unroll
+    for (int s = 0; s < KMAX; ++s)
+      if (s < q) rc_[2 + s] = ps[s];
+  }
+}
+
+}  // namespace spx

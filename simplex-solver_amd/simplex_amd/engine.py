@@ -301,6 +301,19 @@ class DeviceTableau:
         """Windowed elimination: K pivots per pass over the tableau (0/1 = off)."""
         self._check(self._lib.spx_set_window(self._ctx, int(K)), "spx_set_window")
 
+    def set_chain(self, mode: int = 0, min_blocks: int = 0) -> None:
+        """Pivot chain of a window: 0 = one persistent launch per window when
+        the tableau fits (default), 1 = two launches per pivot (lazy kernels).
+        Bit-identical either way; min_blocks raises the persistent grid."""
+        self._check(self._lib.spx_set_chain(self._ctx, int(mode), int(min_blocks)),
+                    "spx_set_chain")
+
+    def chain_blocks(self) -> int:
+        """Blocks of the persistent chain for the loaded tableau (0: not used)."""
+        b = ctypes.c_int()
+        self._check(self._lib.spx_get_chain(self._ctx, ctypes.byref(b)), "spx_get_chain")
+        return int(b.value)
+
     def set_ld_pad(self, pad: int) -> None:
         """Extra doubles per stored column, applied at the next load."""
         self._check(self._lib.spx_set_ld_pad(self._ctx, int(pad)), "spx_set_ld_pad")

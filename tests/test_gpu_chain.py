@@ -1,0 +1,164 @@
+"""The persistent pivot chain (spx_set_chain, csrc/spx_chain.hpp): one launch
+runs a window's K pivot choices, with in-launch record exchanges instead of two
+launches per pivot.  It must be BYTE-identical to the launch-per-phase chain
+(mode 1) and to the single-pivot engine: pivot sequence, basis, status and the
+tableau (tobytes), and np.array_equal to the CPU oracle.
+"""
+import threading
+
+import numpy as np
+import pytest
+
+from oracle import simplex_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def eng_cls():
+    from simplex_amd.engine import DeviceTableau
+    return DeviceTableau
+
+
+def _random_tableau(rows, cols, seed, zero_frac=0.1):
+    rng = np.random.default_rng(seed)
+    m = rows - 1
+    n = max(1, cols - 1 - m)
+    A = rng.uniform(0.05, 1.0, size=(m, n))
+    A[rng.random(A.shape) < zero_frac] = 0.0
+    T = np.zeros((m + 1, n + m + 1))
+    T[:m, :n] = A
+    T[np.arange(m), n + np.arange(m)] = 1.0
+    T[:m, -1] = rng.uniform(1, 2, size=m) * n
+    T[m, :n] = -rng.uniform(0.1, 1, size=n)
+    return T, np.arange(n, n + m, dtype=np.int64)
+
+
+def _run(eng_cls, T, basis, K, mode, min_blocks=0, **kw):
+    with eng_cls(0) as e:
+        e.set_window(K)
+        e.set_chain(mode, min_blocks)
+        e.load(T, basis)
+        blocks = e.chain_blocks()
+        res = e.solve(**kw)
+        return res, e.history().tolist(), e.tableau(), e.basis(), blocks
+
+
+@pytest.mark.parametrize("K", [2, 8, 16, 24, 32])
+@pytest.mark.parametrize("shape", [(2, 3), (17, 40), (300, 700), (1025, 2051)])
+@pytest.mark.parametrize("rule", ["dantzig", "bland"])
+@pytest.mark.parametrize("mode", [2, 3], ids=["cb256", "cb512"])
+def test_chain_matches_lazy_chain_and_oracle(eng_cls, K, shape, rule, mode):
+    T, basis = _random_tableau(*shape, seed=shape[0] * 7 + K)
+    kw = dict(max_iters=3 * K + 5, rule=rule)
+    res, h, out, b, blocks = _run(eng_cls, T, basis, K, mode, **kw)
+    res1, h1, out1, b1, blocks1 = _run(eng_cls, T, basis, K, 1, **kw)
+    assert blocks >= 1 and blocks1 == 0
+    assert h == h1 and res.status == res1.status and res.iters == res1.iters
+    assert out.tobytes() == out1.tobytes() and np.array_equal(b, b1)
+    ref, rb = T.copy(), basis.copy()
+    st, hist = O.solve_tableau(ref, rb, rule=rule, max_iters=3 * K + 5)
+    assert [tuple(x) for x in h] == hist and res.status == st
+    assert np.array_equal(out, ref) and np.array_equal(b, rb)
+
+
+@pytest.mark.parametrize("min_blocks", [0, 3, 64, 100, 256])
+def test_chain_grid_sizes_bit_exact(eng_cls, min_blocks):
+    """More blocks than the minimum (fewer columns / rows per block, more than
+    64 records per poll) give the same bytes."""
+    T, basis = _random_tableau(400, 1300, seed=11 + min_blocks)
+    res, h, out, b, blocks = _run(eng_cls, T, basis, 16, 0, min_blocks, max_iters=53)
+    res1, h1, out1, b1, _ = _run(eng_cls, T, basis, 16, 1, max_iters=53)
+    assert blocks == max(min_blocks, 6)
+    assert h == h1 and res.iters == res1.iters and out.tobytes() == out1.tobytes()
+
+
+@pytest.mark.parametrize("mode,nb", [(0, 80), (2, 80), (3, 40)])
+def test_chain_wide_tableau_more_than_64_blocks(eng_cls, mode, nb):
+    """N > 64 x 256 columns: B = 80 blocks of 256 threads (two records per
+    polling lane; the automatic choice), or 40 of 512."""
+    T, basis = _random_tableau(301, 20400, seed=5)
+    res, h, out, b, blocks = _run(eng_cls, T, basis, 24, mode, max_iters=60)
+    assert blocks == nb
+    res1, h1, out1, b1, _ = _run(eng_cls, T, basis, 24, 1, max_iters=60)
+    assert h == h1 and out.tobytes() == out1.tobytes() and np.array_equal(b, b1)
+
+
+@pytest.mark.parametrize("K", [4, 32])
+def test_chain_degenerate_bland_full_solve(eng_cls, K):
+    from simplex_amd import synth
+    T, basis = synth.full_tableau("degenerate", 96, 96, seed=3)
+    res, h, out, b, _ = _run(eng_cls, T, basis, K, 0, rule="bland")
+    res1, h1, out1, b1, _ = _run(eng_cls, T, basis, K, 1, rule="bland")
+    ref, rb = T.copy(), basis.copy()
+    st, hist = O.solve_tableau(ref, rb, rule="bland")
+    assert res.status == res1.status == st == 0
+    assert [tuple(x) for x in h] == hist == [tuple(x) for x in h1]
+    assert out.tobytes() == out1.tobytes() and np.array_equal(out, ref)
+
+
+def test_chain_stops_inside_window(eng_cls):
+    """Optimal, unbounded and the iteration limit inside a window."""
+    # optimal after a few pivots
+    T, basis = _random_tableau(30, 80, seed=9)
+    for mi in (0, 5, 13):
+        r0 = _run(eng_cls, T, basis, 32, 0, max_iters=mi)
+        r1 = _run(eng_cls, T, basis, 32, 1, max_iters=mi)
+        assert r0[0].status == r1[0].status and r0[1] == r1[1]
+        assert r0[2].tobytes() == r1[2].tobytes()
+    # unbounded: a column with no positive entry enters
+    T2, b2 = _random_tableau(20, 50, seed=4)
+    n = 50 - 1 - 19
+    T2[:19, 3] = -np.abs(T2[:19, 3]) - 0.1
+    T2[19, 3] = -50.0
+    r0 = _run(eng_cls, T2, b2, 8, 0)
+    r1 = _run(eng_cls, T2, b2, 8, 1)
+    ref, rb = T2.copy(), b2.copy()
+    st, hist = O.solve_tableau(ref, rb)
+    assert r0[0].status == r1[0].status == st == 3
+    assert r0[1] == r1[1] == [list(x) for x in hist]
+    assert r0[2].tobytes() == r1[2].tobytes()
+    del n
+
+
+def test_chain_resume_across_calls(eng_cls):
+    """Several calls on one context (iteration limits mid-window, pivot_at)."""
+    T, basis = _random_tableau(200, 600, seed=21)
+    outs = []
+    for mode in (0, 1):
+        with eng_cls(0) as e:
+            e.set_window(16)
+            e.set_chain(mode)
+            e.load(T, basis)
+            e.solve(max_iters=7)
+            e.solve(max_iters=20)
+            e.pivot()
+            e.solve(max_iters=30)
+            outs.append((e.history().tolist(), e.tableau().tobytes(), e.basis().tolist()))
+    assert outs[0] == outs[1]
+
+
+def test_chain_concurrent_contexts(eng_cls):
+    """Two contexts' persistent chains on two streams at once."""
+    T, basis = _random_tableau(500, 1500, seed=33)
+    res = [None, None]
+
+    def work(k):
+        res[k] = _run(eng_cls, T, basis, 24, 0, max_iters=100)
+
+    th = [threading.Thread(target=work, args=(k,)) for k in range(2)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    ref = _run(eng_cls, T, basis, 24, 1, max_iters=100)
+    for r in res:
+        assert r[1] == ref[1] and r[2].tobytes() == ref[2].tobytes()
+
+
+def test_chain_set_validated(eng_cls):
+    with eng_cls(0) as e:
+        with pytest.raises(Exception):
+            e.set_chain(4)
+        with pytest.raises(Exception):
+            e.set_chain(0, 300)

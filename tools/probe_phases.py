@@ -33,6 +33,7 @@ def main():
     ap.add_argument("--n", type=int, default=8192)
     ap.add_argument("--build-only", action="store_true")
     ap.add_argument("--fv", type=int, default=0)
+    ap.add_argument("--chain", type=int, default=0, help="0 persistent chain, 1 lazy kernels")
     a = ap.parse_args()
     if a.build_only or not os.path.exists(LIB):
         build()
@@ -46,6 +47,7 @@ def main():
     Tf, obj, basis = synth.tableau_rows("dense", a.m, a.n, 20251205, order="F")
     e = DeviceTableau(0)
     e.set_window(K)
+    e.set_chain(a.chain)
     e.load_rows(Tf, obj, basis, a.m, 0)
     e.set_elim_variant(0, 0, -1, flush_variant=a.fv & 7, flush_map=a.fv >> 3)
     del Tf
@@ -60,7 +62,8 @@ def main():
     t = lambda slot, kind, ph: buf[((slot * 4 + kind) * 4 + ph) & 1023]
     t0 = t(0, 0, 0)
     us = lambda x: (x - t0) / 100.0
-    names = {0: "lazy_ratio", 1: "lazy_norm"}
+    names = ({0: "lazy_ratio", 1: "lazy_norm"} if a.chain else
+             {0: "ratio ph.", 1: "norm ph."})
     print(f"window K={K}, m={a.m}, n={a.n}: us from lazy_ratio(0) entry (block 0, thread 0)")
     prev_end = None
     for q in range(K):
@@ -74,6 +77,22 @@ def main():
             if kind == 0 and os.environ.get("SPX_PROBE_FINE"):
                 k0, k1 = us(t(q, 2, 0)), us(t(q, 2, 1))
                 print(f"       fine: keys reduced +{k0 - ph[0]:5.2f}  wave_min +{k1 - k0:5.2f}")
+    if not a.chain:
+        nb = e.chain_blocks()
+        cb = (ctypes.c_ulonglong * (32 * 4 * 256))()
+        assert lib.spx_probe_read_chain(cb, 32 * 4 * 256) == 0
+        ev = lambda q, k: [(cb[(q * 4 + k) * 256 + x] - t0) / 100.0 for x in range(nb)]
+        import statistics as S
+        print(f"per-block exchange timing ({nb} blocks), us: publish spread = last - first "
+              "record stored; seen = poll done - last record stored (min / median / max)")
+        for q in range(1, K - 1):
+            for name, pub, see in (("ratio", 0, 1), ("enter", 2, 3)):
+                P_, D_ = ev(q, pub), ev(q, see)
+                last = max(P_)
+                seen = [d - last for d in D_]
+                print(f"  q={q:2d} {name}: publish spread {last - min(P_):5.2f} "
+                      f"(block 0 at {P_[0] - min(P_):5.2f}, slowest block {P_.index(last):3d})  "
+                      f"seen {min(seen):5.2f} / {S.median(seen):5.2f} / {max(seen):5.2f}")
     f0, f1 = us(t(K, 2, 0)), us(t(K, 2, 1))
     print(f"flush entry {f0:8.2f} (+{f0 - prev_end:5.2f})  block-0 duration {f1 - f0:7.2f}")
     rch, G = ctypes.c_int(), ctypes.c_int()
