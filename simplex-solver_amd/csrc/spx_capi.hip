@@ -132,8 +132,6 @@ struct spx_ctx {
   // persistent pivot chain of a window (spx_chain.hpp): record buffers and mode
   unsigned long long* gr_enter = nullptr;  // ENTER_REC x CHAIN_MAX_BLOCKS granules
   unsigned long long* gr_ratio = nullptr;  // RATIO_REC x CHAIN_MAX_BLOCKS granules
-  unsigned long long* pg = nullptr;        // N x KW x 2 history granules of p_s[j]
-  unsigned long long* fg = nullptr;        // m x KW x 2 history granules of f_s[i]
   int chain_mode = 0;      // 0: persistent chain when it fits, 1: launch per phase
   int chain_min_blocks = 0;
 
@@ -211,8 +209,6 @@ int free_buffers(spx_ctx* ctx) {
   dfree(ctx->win.rec);
   dfree(ctx->gr_enter);
   dfree(ctx->gr_ratio);
-  dfree(ctx->pg);
-  dfree(ctx->fg);
   ctx->loaded = false;
   return SPX_OK;
 }
@@ -414,8 +410,7 @@ int enqueue_window_t(spx_ctx* ctx, int npiv, bool time_flush) {
     hipLaunchKernelGGL(kern, dim3(B), dim3(cb), 0, ctx->stream, ctx->enter_part, ctx->st,
                        (const Params*)ctx->prm, std::max(NWAVE * ctx->nbn, B),
                        (const double*)ctx->A, ctx->ld, ctx->m_local, ctx->N, ctx->obj, ctx->win,
-                       npiv, ctx->basis, ctx->hist, ctx->gr_enter, ctx->gr_ratio, ctx->pg,
-                       ctx->fg, cpb, rpb);
+                       npiv, ctx->basis, ctx->hist, ctx->gr_enter, ctx->gr_ratio, cpb, rpb);
   }
   for (int q = 0; B == 0 && q < npiv; ++q) {
     hipLaunchKernelGGL(lazy_ratio_kernel<KMAX>, dim3(nbw), dim3(BLK), 0, ctx->stream,
@@ -701,12 +696,6 @@ int alloc_common(spx_ctx* ctx, int64_t m_local, int64_t N, int64_t m_global, int
     HIPC(hipMalloc(&ctx->gr_ratio, gq));
     HIPC(hipMemsetAsync(ctx->gr_enter, 0, ge, ctx->stream));
     HIPC(hipMemsetAsync(ctx->gr_ratio, 0, gq, ctx->stream));
-    const size_t gp = sizeof(unsigned long long) * 2 * KW * N;
-    const size_t gf = sizeof(unsigned long long) * 2 * KW * std::max<int64_t>(1, m_local);
-    HIPC(hipMalloc(&ctx->pg, gp));
-    HIPC(hipMalloc(&ctx->fg, gf));
-    HIPC(hipMemsetAsync(ctx->pg, 0, gp, ctx->stream));
-    HIPC(hipMemsetAsync(ctx->fg, 0, gf, ctx->stream));
   }
   if (ctx->sharded) {
     ctx->gstride = round_up(PAYLOAD_HDR + (int64_t)sizeof(double) * N, 256);

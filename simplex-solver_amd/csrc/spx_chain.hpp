@@ -64,14 +64,13 @@ constexpr int32_t ST_FAULT = 5;       // a chain exchange timed out (never on a 
 // Records are stored granule-major: granule g of block b at rec[g * CHAIN_MAX_BLOCKS + b],
 // so one poll instruction of a wave reads 64 blocks' granule g as 512 contiguous bytes.
 // A record is a polled header plus extras that only the winner's record is read for
-// (after the poll, beside the phase's other dependent loads); the extras carry the
-// values computed in the same phase as the record, so no consumer waits on a
-// history granule stored moments before the header.
-constexpr int ENTER_REC = 5;          // o_lo, o_hi, j | extras: p_q[j] lo, hi
-constexpr int ENTER_HDR = 3;
-constexpr int RATIO_REC = 8;          // v_lo, v_hi, row, t (Bland only) | extras: f_q[row] lo, hi,
-constexpr int RATIO_HDR = 4;          //   RHS of row lo, hi
-constexpr int CHAIN_MAX_BLOCKS = 256; // one block per CU
+// (after the poll, beside the phase's other dependent loads): the winning row's or
+// column's whole window history, so no other history is ever stored write-through.
+constexpr int ENTER_HDR = 3;            // o_lo, o_hi, j
+constexpr int ENTER_REC = ENTER_HDR + 2 * 32;  // + p_0..p_q[j] (lo, hi each)
+constexpr int RATIO_HDR = 4;            // v_lo, v_hi, row, t (t read under Bland only)
+constexpr int RATIO_REC = RATIO_HDR + 2 + 2 * 32;  // + RHS of row (lo, hi), f_0..f_q[row]
+constexpr int CHAIN_MAX_BLOCKS = 256;   // one block per CU
 constexpr unsigned CHAIN_SPIN_MAX = 1u << 22;
 
 typedef __attribute__((address_space(1))) unsigned long long gu64;
@@ -99,8 +98,6 @@ __device__ __forceinline__ void drain_stores() { asm volatile("s_waitcnt vmcnt(0
 // granule kinds
 constexpr int GK_RATIO = 0;  // ratio record of slot q
 constexpr int GK_ENTER = 1;  // entering record published by slot q (for slot q+1)
-constexpr int GK_PHIST = 2;  // p_q[j] of a column (history granules)
-constexpr int GK_FHIST = 3;  // f_q[i] of a row (history granules)
 // granule tag: never 0 (the buffers start zeroed), unique per (epoch, slot, kind)
 __device__ __forceinline__ unsigned rec_tag(uint32_t epoch, int q, int kind) {
   return 0x80000000u | ((epoch & 0x7fffffu) << 8) | ((unsigned)q << 2) | (unsigned)kind;
@@ -155,18 +152,58 @@ __device__ __forceinline__ void wave_min2(KeyP& k) {
   kmin2_swap<16>(k);
   kmin2_swap<32>(k);
 }
-// Block argmin (+ payload) of NW waves into thread 0.  All threads must call it.
-template <int NW>
-__device__ __forceinline__ void block_min2(KeyP& k) {
-  __shared__ KeyP sk[NW];
-  wave_min2(k);
-  const int w = threadIdx.x >> 6;
-  if ((threadIdx.x & 63) == 0) sk[w] = k;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-#pragma unroll
-    for (int x = 1; x < NW; ++x) kmin2(k, sk[x].v, sk[x].t, sk[x].row, sk[x].a, sk[x].b);
+// Wave argmin of (v, t), lexicographic, by value first: a DPP min of v, then
+// the lanes holding it by ballot.  When t grows with the lane index among the
+// lanes (t_mono) the lowest such lane wins; otherwise a DPP min of t among the
+// tied lanes picks it.  Returns the winning lane (wave-uniform) or -1 when no
+// lane is valid.  About a fifth of wave_min2's instructions.
+template <int CTRL>
+__device__ __forceinline__ double dpp_minf(double x) {
+  return fmin(x, dbits(dpp64<CTRL>(ibits(x))));
+}
+template <int D>
+__device__ __forceinline__ double swap_minf(double x) {
+  return fmin(x, dbits(swap64<D>(ibits(x))));
+}
+__device__ __forceinline__ double wave_minf(double x) {
+  x = dpp_minf<0x128>(x);
+  x = dpp_minf<0x124>(x);
+  x = dpp_minf<0x4E>(x);
+  x = dpp_minf<0xB1>(x);
+  x = swap_minf<16>(x);
+  return swap_minf<32>(x);
+}
+template <int CTRL>
+__device__ __forceinline__ int64_t dpp_mini(int64_t x) {
+  const int64_t y = dpp64<CTRL>(x);
+  return y < x ? y : x;
+}
+template <int D>
+__device__ __forceinline__ int64_t swap_mini(int64_t x) {
+  const int64_t y = swap64<D>(x);
+  return y < x ? y : x;
+}
+__device__ __forceinline__ int wave_argmin(double v, int64_t t, bool valid, bool t_mono) {
+  const double vmin = wave_minf(valid ? v : __builtin_inf());
+  uint64_t tie = __ballot(valid && v == vmin);
+  if (tie == 0ull) return -1;
+  if (!t_mono && __popcll(tie) > 1) {
+    int64_t x = ((tie >> (threadIdx.x & 63)) & 1ull) ? t : INT64_MAX;
+    x = dpp_mini<0x128>(x);
+    x = dpp_mini<0x124>(x);
+    x = dpp_mini<0x4E>(x);
+    x = dpp_mini<0xB1>(x);
+    x = swap_mini<16>(x);
+    x = swap_mini<32>(x);
+    tie = __ballot(((tie >> (threadIdx.x & 63)) & 1ull) && t == x);
   }
+  return (int)__builtin_ctzll(tie);
+}
+// the winning lane's key and payload, to every lane
+__device__ __forceinline__ KeyP key_of_lane(const KeyP& k, int ln) {
+  if (ln < 0) return keyp_none();
+  return KeyP{rdlane(k.v, ln), rdlane64(k.t, ln), rdlane64(k.row, ln), rdlane(k.a, ln),
+              rdlane(k.b, ln)};
 }
 
 // Bounded spin bookkeeping: true (and ST_FAULT stored) once a wait ran too long.
@@ -203,96 +240,74 @@ __device__ __forceinline__ void decode_record(KeyP& k, const unsigned long long 
   }
 }
 
-template <bool RATIO, int G>
-__device__ __forceinline__ bool poll_records(const gu64* recs, int B, unsigned tag, int rule,
-                                             KeyP& k, State* st) {
+template <bool RATIO, int G, int RPL>
+__device__ __forceinline__ bool poll_records_n(const gu64* recs, int B, unsigned tag, int rule,
+                                               KeyP& k, State* st) {
   const int lane = threadIdx.x & 63;
-  const unsigned long long none = (unsigned long long)tag << 32;
-  if (B <= 64) {
-    // one record per lane: three passes in flight, staggered, so a record is
-    // seen about one load latency after it lands instead of up to two
-    const bool live = lane < B;
-    const gu64* r = recs + (live ? lane : 0);  // (idle lanes re-read block 0: no branch)
-    unsigned long long x0[4], x1[4], x2[4];
-    auto issue = [&](unsigned long long (&g)[4]) {
+  // lane l reads blocks l, l+64, ... (RPL records): every load of a pass is
+  // issued before the first tag check, so a pass is one round trip (one pass
+  // in flight: more passes measured slower, tools/chain_probe.hip)
+  for (unsigned spins = 0;;) {
+    unsigned long long g[RPL][4];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) g[u] = u < G ? g_load(r + (size_t)u * CHAIN_MAX_BLOCKS) : none;
-    };
-    auto good = [&](const unsigned long long (&g)[4]) {
-      bool ok = true;
+    for (int x = 0; x < RPL; ++x) {
+      const int b = min(lane + 64 * x, B - 1);  // clamped: no branch around the loads
 #pragma unroll
-      for (int u = 0; u < 4; ++u) ok &= (unsigned)(g[u] >> 32) == tag;
-      return __all(ok);
-    };
-    issue(x0);
-    __builtin_amdgcn_s_sleep(8);
-    issue(x1);
-    __builtin_amdgcn_s_sleep(8);
-    issue(x2);
-    int hit;
-    for (unsigned spins = 0;; ++spins) {
-      if (good(x0)) { hit = 0; break; }
-      issue(x0);
-      if (good(x1)) { hit = 1; break; }
-      issue(x1);
-      if (good(x2)) { hit = 2; break; }
-      issue(x2);
-      if (spins >= CHAIN_SPIN_MAX / 4) {
-        if (lane == 0)
-          __hip_atomic_store((gu32*)&st->status, (unsigned)ST_FAULT, __ATOMIC_RELAXED,
-                             __HIP_MEMORY_SCOPE_AGENT);
-        return false;
-      }
+      for (int u = 0; u < 4; ++u)
+        g[x][u] = u < G ? g_load(recs + (size_t)u * CHAIN_MAX_BLOCKS + b)
+                        : (unsigned long long)tag << 32;
     }
-    k = keyp_none();
-    unsigned long long g[4];
+    bool ok = true;
 #pragma unroll
-    for (int u = 0; u < 4; ++u) g[u] = hit == 0 ? x0[u] : hit == 1 ? x1[u] : x2[u];
-    if (live) decode_record<RATIO>(k, g, lane, rule);
-  } else {
-    for (unsigned spins = 0;;) {
-      bool ok = true;
+    for (int x = 0; x < RPL; ++x)
+#pragma unroll
+      for (int u = 0; u < 4; ++u) ok &= (unsigned)(g[x][u] >> 32) == tag;
+    if (__all(ok)) {
       k = keyp_none();
-      for (int b = lane; b < B; b += 64) {
-        unsigned long long g[4];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) g[u] = u < G ? g_load(recs + (size_t)u * CHAIN_MAX_BLOCKS + b) : none;
-#pragma unroll
-        for (int u = 0; u < 4; ++u) ok &= (unsigned)(g[u] >> 32) == tag;
-        decode_record<RATIO>(k, g, b, rule);
-      }
-      if (__all(ok)) break;
-      if (spin_fail(spins, st)) return false;
+      for (int x = 0; x < RPL; ++x)
+        if (lane + 64 * x < B) decode_record<RATIO>(k, g[x], lane + 64 * x, rule);
+      break;
     }
+    if (spin_fail(spins, st)) return false;
   }
-  wave_min2(k);
+  // one record per lane: lane order is block order, and a block's rows and
+  // columns all precede the next block's, so t grows with the lane except for
+  // Bland's ratio key (a basic-variable index)
+  const bool mono = RPL == 1 && !(RATIO && rule == RULE_BLAND);
+  k = key_of_lane(k, wave_argmin(k.v, k.t, k.row >= 0, mono));
   asm volatile("" ::: "memory");  // the loads that follow must not be hoisted above the poll
   return true;
 }
 
-// The dependent loads of a phase: lane s < n reads history slot s of one
-// column / row (granules h[2s], h[2s+1], tag of slot s), and every lane reads
-// NE doubles of extras (granule pairs at e + 2x*CHAIN_MAX_BLOCKS, tag etag).
-// One pass re-reads until every granule matches.  Returns false on timeout.
+template <bool RATIO, int G>
+__device__ __forceinline__ bool poll_records(const gu64* recs, int B, unsigned tag, int rule,
+                                             KeyP& k, State* st) {
+  if (B <= 64) return poll_records_n<RATIO, G, 1>(recs, B, tag, rule, k, st);
+  if (B <= 128) return poll_records_n<RATIO, G, 2>(recs, B, tag, rule, k, st);
+  return poll_records_n<RATIO, G, 4>(recs, B, tag, rule, k, st);
+}
+
+// The dependent loads of a phase from the winning record (block wb): lane
+// s < n reads the history pair at planes h0 + 2s, h0 + 2s + 1, and every lane
+// reads NE wave-uniform pairs at planes e0 + 2x.  One pass re-reads until every
+// granule carries the record's tag.  Returns false on timeout.
 template <int NE>
-__device__ __forceinline__ bool load_phase(const gu64* h, int n, uint32_t W, int kind,
-                                           const gu64* e, unsigned etag, double& hv,
-                                           double (&ev)[2], State* st) {
+__device__ __forceinline__ bool load_extras(const gu64* rec, int wb, int h0, int n, int e0,
+                                            unsigned tag, double& hv, double (&ev)[2],
+                                            State* st) {
   const int lane = threadIdx.x & 63;
   const bool mine = lane < n;
-  const unsigned tag = rec_tag(W, lane, kind);
-  const gu64* g = h + 2 * (mine ? lane : 0);
+  const gu64* g = rec + (size_t)(h0 + 2 * (mine ? lane : 0)) * CHAIN_MAX_BLOCKS + wb;
+  const gu64* e = rec + (size_t)e0 * CHAIN_MAX_BLOCKS + wb;
   for (unsigned spins = 0;;) {
-    unsigned long long lo = 0, hi = 0, x[2 * NE > 0 ? 2 * NE : 1];
-    if (mine) {
-      lo = g_load(g);
-      hi = g_load(g + 1);
-    }
+    const unsigned long long lo = g_load(g), hi = g_load(g + CHAIN_MAX_BLOCKS);
+    unsigned long long x[2 * NE > 0 ? 2 * NE : 1];
 #pragma unroll
     for (int u = 0; u < 2 * NE; ++u) x[u] = g_load(e + (size_t)u * CHAIN_MAX_BLOCKS);
     bool good = !mine || ((unsigned)(lo >> 32) == tag && (unsigned)(hi >> 32) == tag);
 #pragma unroll
-    for (int u = 0; u < 2 * NE; ++u) good &= (unsigned)(x[u] >> 32) == etag;
+    for (int u = 0; u < 2 * NE; ++u) good &= (unsigned)(x[u] >> 32) == tag;
     if (__all(good)) {
       hv = mine ? g_decode_d(lo, hi) : 0.0;
 #pragma unroll
@@ -303,41 +318,80 @@ __device__ __forceinline__ bool load_phase(const gu64* h, int n, uint32_t W, int
   }
 }
 
+// Publish a block's record: wave w's winning lane has put its history (slots
+// 0..nh-1) and `extra` into hist_lds[w][], the wave keys are in sk[]; after the
+// block barrier wave 0 reduces the NW keys (every lane the same winner), its
+// lanes store the winner's extras, then lane 0 the header (program order: the
+// extras leave first).  RATIO: header v, row, t; extras [extra, history].
+template <int NW, bool RATIO>
+__device__ __forceinline__ void publish_record(gu64* rec, int b, unsigned tag, int nh,
+                                               const KeyP (&sk)[NW], const double (*hl)[34]) {
+  const int lane = threadIdx.x & 63;
+  KeyP k = sk[0];
+#pragma unroll
+  for (int x = 1; x < NW; ++x) kmin2(k, sk[x].v, sk[x].t, sk[x].row, sk[x].a, sk[x].b);
+  const int ww = (int)k.b;  // the winning wave (a payload slot of the block key)
+  const bool none = k.row < 0;
+  gu64* rb = rec + b;
+  constexpr int H0 = RATIO ? RATIO_HDR + 2 : ENTER_HDR;  // first history plane
+  if (!none) {
+    // lane x < 2*nh: history granule x; RATIO: lanes 62, 63 the extra (row's RHS)
+    if (lane < 2 * nh) {
+      const unsigned long long x =
+          (unsigned long long)__double_as_longlong(hl[ww][lane >> 1]);
+      g_store(rb + (size_t)(H0 + lane) * CHAIN_MAX_BLOCKS, tag,
+              (lane & 1) ? (unsigned)(x >> 32) : (unsigned)x);
+    }
+    if (RATIO && lane >= 62) {
+      const unsigned long long x = (unsigned long long)__double_as_longlong(hl[ww][33]);
+      g_store(rb + (size_t)(RATIO_HDR + (lane - 62)) * CHAIN_MAX_BLOCKS, tag,
+              (lane & 1) ? (unsigned)(x >> 32) : (unsigned)x);
+    }
+  }
+  if (lane == 0) {
+    const unsigned long long vb = (unsigned long long)__double_as_longlong(RATIO ? k.v : k.a);
+    g_store(rb + 0 * CHAIN_MAX_BLOCKS, tag, (unsigned)vb);
+    g_store(rb + 1 * CHAIN_MAX_BLOCKS, tag, (unsigned)(vb >> 32));
+    g_store(rb + 2 * CHAIN_MAX_BLOCKS, tag, none ? 0xffffffffu : (unsigned)k.row);
+    if (RATIO) g_store(rb + 3 * CHAIN_MAX_BLOCKS, tag, none ? 0xffffffffu : (unsigned)k.t);
+  }
+}
+
 // ---------------------------------------------------------------------------
 // chain_kernel<KMAX, CB>: the pivots of one window (npiv <= KMAX slots),
 // single GPU (row0 = 0).  grid = B blocks of CB threads (one block per CU,
 // every block resident); block b owns columns [b*cpb, ...) and rows
 // [b*rpb, ...), cpb, rpb <= CB, one of each per thread.  Wave 0 of a block
 // polls the record headers and hands the winner to the block through LDS;
-// every thread then loads what its column / row needs.  n_ep / enter_part:
-// pivot 0's entering partials, written by the previous kernel (norm<INIT> or
-// the previous window's chain); the chain writes one partial per block there
-// for the next window.  pg / fg: history granules of every column / row (2 per
-// slot), read by later phases (the newest slot travels in the records).
+// every thread then loads what its column / row needs (the winning record's
+// history beside the stale tableau value).  n_ep / enter_part: pivot 0's
+// entering partials, written by the previous kernel (norm<INIT> or the
+// previous window's chain); the chain writes one partial per block there for
+// the next window.
 // ---------------------------------------------------------------------------
 template <int KMAX, int CB>
 __global__ __launch_bounds__(CB) void chain_kernel(
     Key* __restrict__ enter_part, State* st, const Params* __restrict__ prm, int n_ep,
     const double* __restrict__ A, int64_t ld, int64_t m, int64_t N, double* __restrict__ obj,
     Window win, int npiv, int64_t* __restrict__ basis, int64_t* __restrict__ hist,
-    unsigned long long* gr_enter_, unsigned long long* gr_ratio_, unsigned long long* pg_,
-    unsigned long long* fg_, int cpb, int rpb) {
+    unsigned long long* gr_enter_, unsigned long long* gr_ratio_, int cpb, int rpb) {
   static_assert(KMAX <= 32, "slots are lane-indexed and fit the window buffers");
   constexpr int NW = CB / 64;
   constexpr int CH = KMAX % 8 == 0 ? 8 : KMAX % 4 == 0 ? 4 : 2;
   // one block per CU: the record protocol is validated for that residency
-  __shared__ double lds_pin[88 * 128];
+  __shared__ double lds_pin[80 * 128];
   __shared__ int64_t bc_idx;  // the winner handed from wave 0 to the block
   __shared__ double bc_val;
   __shared__ int bc_blk;
+  __shared__ KeyP sk[NW];       // the waves' best keys (payload b = wave index)
+  __shared__ double hl[NW][34];  // their winners' histories (+ [33]: the row's RHS)
   gu64* gr_enter = (gu64*)gr_enter_;
   gu64* gr_ratio = (gu64*)gr_ratio_;
-  gu64* pg = (gu64*)pg_;
-  gu64* fg = (gu64*)fg_;
   const int B = gridDim.x;
   const int b = blockIdx.x;
   const int t = threadIdx.x;
   const int lane = t & 63;
+  const int w = t >> 6;
   const bool w0 = t < 64;
   const bool leader = b == 0 && t == 0;
   // --- everything that does not depend on a pivot, in one batch ---
@@ -428,15 +482,13 @@ __global__ __launch_bounds__(CB) void chain_kernel(
     if (c < 0) stop_status = ST_OPTIMAL;
     else if (forced_r < 0 && it >= iter_limit) stop_status = ST_LIMIT;
     if (stop_status != ST_RUNNING) break;  // grid-uniform
-    // column c and the RHS on my row: stale + pending slots, in slot order.
-    // p_s[c]: slots < q-1 from the history granules (lane s), slot q-1 from the
-    // winning entering record's extras
+    // column c on my row: stale + pending slots, in slot order; p_s[c] (lane
+    // s) from the winning entering record's history
     double fv = A[c * ld + ic];
-    double pcl = 0.0, pnew[2] = {0.0, 0.0};
+    double pcl = 0.0, unused[2];
     if (q > 0 &&
-        !load_phase<1>(pg + (size_t)c * 2 * KW, q - 1, W, GK_PHIST,
-                       gr_enter + ENTER_HDR * CHAIN_MAX_BLOCKS + wb, rec_tag(W, q - 1, GK_ENTER),
-                       pcl, pnew, st))
+        !load_extras<0>(gr_enter, wb, ENTER_HDR, q, 0, rec_tag(W, q - 1, GK_ENTER), pcl, unused,
+                        st))
       return;
     // RHS: apply slot q-1 (the slots before it are already in bcur)
     if (q > 0) bcur = apply_sel(bcur, i == r_prev, false, true, f_prev, prhs, skip);
@@ -449,8 +501,7 @@ __global__ __launch_bounds__(CB) void chain_kernel(
           const bool act = s < q;
           const bool isr = i == rdlane64(slot_r, s);
           const bool isc = c == rdlane64(slot_c, s);
-          const double p_s = (s == q - 1) ? pnew[0] : rdlane(pcl, s);
-          fv = apply_sel(fv, isr, isc, act, fs[s], p_s, skip);
+          fv = apply_sel(fv, isr, isc, act, fs[s], rdlane(pcl, s), skip);
         }
       }
     }
@@ -460,30 +511,29 @@ __global__ __launch_bounds__(CB) void chain_kernel(
     KeyP k = keyp_none();
     if (ilive) {
       win.F[(int64_t)q * ld + i] = fv;  // for the flush / row_fix (later kernels)
-      g_store_d(fg + (size_t)i * 2 * KW + 2 * q, rec_tag(W, q, GK_FHIST), fv);
       if (forced_r >= 0) {
-        if (i == forced_r) kmin2(k, 0.0, 0, i, fv, bcur);
+        if (i == forced_r) kmin2(k, 0.0, 0, i, 0.0, 0.0);
       } else if (fv > eps_piv) {
         const double rq = bcur / fv;
-        if (rq == rq) kmin2(k, rq, rule == RULE_BLAND ? bas : i, i, fv, bcur);
+        if (rq == rq) kmin2(k, rq, rule == RULE_BLAND ? bas : i, i, 0.0, 0.0);
       }
     }
     SPX_PROBE(q, 0, 2, fv != 12345.678);
-    block_min2<NW>(k);
-    if (t == 0) {
-      gu64* rr = gr_ratio + b;
-      const unsigned tag = rec_tag(W, q, GK_RATIO);
-      const bool none = k.row < 0;
-      // extras first: f_q[row] (the pivot element) and the row's current RHS
-      g_store_d(rr + 4 * CHAIN_MAX_BLOCKS, tag, k.a, CHAIN_MAX_BLOCKS);
-      g_store_d(rr + 6 * CHAIN_MAX_BLOCKS, tag, k.b, CHAIN_MAX_BLOCKS);
-      const unsigned long long vb = (unsigned long long)__double_as_longlong(k.v);
-      g_store(rr + 0 * CHAIN_MAX_BLOCKS, tag, (unsigned)vb);
-      g_store(rr + 1 * CHAIN_MAX_BLOCKS, tag, (unsigned)(vb >> 32));
-      g_store(rr + 2 * CHAIN_MAX_BLOCKS, tag, none ? 0xffffffffu : (unsigned)k.row);
-      g_store(rr + 3 * CHAIN_MAX_BLOCKS, tag, none ? 0xffffffffu : (unsigned)k.t);
+    // publish: the wave winner puts its f history and RHS in LDS, the block's
+    // winner is published by wave 0 (rows grow with the lane: Dantzig's tie key)
+    k = key_of_lane(k, wave_argmin(k.v, k.t, k.row >= 0, rule != RULE_BLAND));
+    if (ilive && k.row == i) {
+#pragma unroll
+      for (int s = 0; s < KMAX; ++s)
+        if (s <= q) hl[w][s] = fs[s];
+      hl[w][33] = bcur;
     }
-    SPX_PROBE_CHAIN(q, 0);
+    if (lane == 0) sk[w] = KeyP{k.v, k.t, k.row, 0.0, (double)w};
+    __syncthreads();
+    if (w0) {
+      publish_record<NW, true>(gr_ratio, b, rec_tag(W, q, GK_RATIO), q + 1, sk, hl);
+      SPX_PROBE_CHAIN(q, 0);
+    }
     SPX_PROBE(q, 0, 3, true);
     // ================= norm phase q =================
     SPX_PROBE(q, 1, 0, true);
@@ -509,16 +559,15 @@ __global__ __launch_bounds__(CB) void chain_kernel(
       stop_status = ST_UNBOUNDED;
       break;
     }
-    // row r on my column: stale + pending slots.  f_s[r] for s < q from the
-    // history granules (lane s); the pivot element f_q[r] and the row's RHS
-    // from the winning ratio record's extras
+    // row r on my column: stale + pending slots.  f_s[r] (lane s <= q, lane q
+    // the pivot element) and the row's RHS from the winning ratio record
     double v = A[jc * ld + r];
     double frl = 0.0, ex[2];
-    if (!load_phase<2>(fg + (size_t)r * 2 * KW, q, W, GK_FHIST,
-                       gr_ratio + 4 * CHAIN_MAX_BLOCKS + wb, rec_tag(W, q, GK_RATIO), frl, ex, st))
+    if (!load_extras<1>(gr_ratio, wb, RATIO_HDR + 2, q + 1, RATIO_HDR, rec_tag(W, q, GK_RATIO),
+                        frl, ex, st))
       return;
-    const double piv = ex[0];
-    prhs = ex[1] / piv;  // p_q[rhs]: lazy_norm's p = v / piv of the RHS column
+    const double piv = rdlane(frl, q);
+    prhs = ex[0] / piv;  // p_q[rhs]: lazy_norm's p = v / piv of the RHS column
     bool zb = false;
 #pragma unroll
     for (int c8 = 0; c8 < KMAX; c8 += CH) {
@@ -540,7 +589,6 @@ __global__ __launch_bounds__(CB) void chain_kernel(
 #pragma unroll
       for (int s = 0; s < KMAX; ++s) ps[s] = (s == q) ? p : ps[s];
       win.P[j * KW + q] = p;  // for row_fix (a later kernel)
-      g_store_d(pg + (size_t)j * 2 * KW + 2 * q, rec_tag(W, q, GK_PHIST), p);
       const bool nz = (p != 0.0) || !skip;
       if (j == c) {
         o = 0.0;
@@ -554,8 +602,8 @@ __global__ __launch_bounds__(CB) void chain_kernel(
       } else if (tagged) {
         tg = tg | TAG_ZERO;
       }
-      // key (o, j) under Dantzig, (0, j) under Bland; payload o (z_c) and p_q[j]
-      if (j < n_enter && o < -eps_opt) kmin2(ek, rule == RULE_BLAND ? 0.0 : o, j, j, o, p);
+      // key (o, j) under Dantzig, (0, j) under Bland; payload o (z_c)
+      if (j < n_enter && o < -eps_opt) kmin2(ek, rule == RULE_BLAND ? 0.0 : o, j, j, o, 0.0);
     }
     if (ilive && i == r) bas = c;
     if (lane == q) {
@@ -578,19 +626,23 @@ __global__ __launch_bounds__(CB) void chain_kernel(
       }
     }
     SPX_PROBE(q, 1, 2, v != 12345.678);
-    block_min2<NW>(ek);
-    if (t == 0) {
+    ek = key_of_lane(ek, wave_argmin(ek.v, ek.t, ek.row >= 0, true));  // columns grow with the lane
+    if (q + 1 < npiv && jlive && ek.row == j) {
+#pragma unroll
+      for (int s = 0; s < KMAX; ++s)
+        if (s <= q) hl[w][s] = ps[s];
+    }
+    if (lane == 0) sk[w] = KeyP{ek.v, ek.t, ek.row, ek.a, (double)w};
+    __syncthreads();
+    if (w0) {
       if (q + 1 < npiv) {
-        gu64* er = gr_enter + b;
-        const unsigned tag = rec_tag(W, q, GK_ENTER);
-        g_store_d(er + ENTER_HDR * CHAIN_MAX_BLOCKS, tag, ek.b, CHAIN_MAX_BLOCKS);  // extras: p_q[j]
-        const unsigned long long ob = (unsigned long long)__double_as_longlong(ek.a);
-        g_store(er + 0 * CHAIN_MAX_BLOCKS, tag, (unsigned)ob);
-        g_store(er + 1 * CHAIN_MAX_BLOCKS, tag, (unsigned)(ob >> 32));
-        g_store(er + 2 * CHAIN_MAX_BLOCKS, tag, ek.row < 0 ? 0xffffffffu : (unsigned)ek.row);
-      } else {
+        publish_record<NW, false>(gr_enter, b, rec_tag(W, q, GK_ENTER), q + 1, sk, hl);
+      } else if (t == 0) {
         // the next window's pivot-0 partial (read after the kernel boundary)
-        store_key(enter_part + b, KeyR{ek.v, ek.t, ek.row});
+        KeyP kb = sk[0];
+#pragma unroll
+        for (int x = 1; x < NW; ++x) kmin2(kb, sk[x].v, sk[x].t, sk[x].row, sk[x].a, sk[x].b);
+        store_key(enter_part + b, KeyR{kb.v, kb.t, kb.row});
       }
       SPX_PROBE_CHAIN(q, 2);
     }
@@ -613,7 +665,6 @@ __global__ __launch_bounds__(CB) void chain_kernel(
   __shared__ int wcnt[NW];
   __shared__ int base;
   const uint64_t bal = __ballot(mine);
-  const int w = t >> 6;
   if (lane == 0) wcnt[w] = __popcll(bal);
   __syncthreads();
   if (t == 0) {
