@@ -75,7 +75,7 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=15.0,
                     help="budget of the CPU-baseline sample (0 disables)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles",
-                                                           "traffic_r01.json"))
+                                                           "traffic_r02.json"))
     return ap.parse_args()
 
 
