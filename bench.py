@@ -56,7 +56,7 @@ def parse():
     ap.add_argument("--fv", type=int, default=-1,
                     help="windowed flush: variant (bits 0-2: 0 LDS-DMA ring of 12, the default; "
                          "6/7 rings of 9/10; 1-5 register rings, power-of-two K only) + 8 x block "
-                         "map (bits 3-4: 1 chunk-major, 2 groups rotated); -1 default")
+                         "map (bits 3-5: 1 chunk-major, 2 groups rotated, 4 dynamic column claims); -1 default")
     ap.add_argument("--graph", type=int, default=1,
                     help="1: the timed region replays one hipGraph with an event pair "
                          "captured around every elimination; 0: direct launches + events")
@@ -186,10 +186,10 @@ def main():
         fv = max(args.fv, 0)
         if args.ilv >= 0:
             eng.set_elim_variant(args.R, args.wgs, -1 if args.nt < 0 else args.nt,
-                                 args.ilv | (fv & 7) << 8 | (fv >> 3 & 3) << 11)
+                                 args.ilv | (fv & 7) << 8 | (fv >> 3 & 7) << 11)
         else:
             eng.set_elim_variant(args.R, args.wgs, -1 if args.nt < 0 else args.nt,
-                                 flush_variant=fv & 7, flush_map=fv >> 3 & 3)
+                                 flush_variant=fv & 7, flush_map=fv >> 3 & 7)
     opts = dict(rule=args.rule, skip_zero_cols=not args.dense, use_graph=use_graph, chunk=32)
 
     def barrier():
@@ -261,6 +261,8 @@ def main():
             kname = "spx::elim_kernel"
         elif fvar["flush_var"] in (1, 2, 3, 4, 5) and pow2:
             kname = "spx::flush_kernel"
+        elif fvar["flush_var"] in (0, 1, 2, 3, 4, 5) and fvar["flush_map"] & 4:
+            kname = "spx::flush_dyn_kernel"
         else:
             kname = "spx::flush_lds_kernel"
         line = {

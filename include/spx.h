@@ -170,13 +170,14 @@ int spx_elim_timing(spx_ctx* ctx, double* total_ms, int64_t* count, int64_t* tou
  * ranges), bit 1 = disable software pipelining of column pairs, bit 2 = XCD-aware
  * block swizzle, bits 8-10 = window flush variant (0 = LDS-DMA ring of 12, the
  * default; 6 / 7 = rings of 9 / 10; 1-5 = register rings, power-of-two K only),
- * bits 11-12 = window flush block map (bit 11 chunk-major, bit 12 group rotated
- * by row chunk; 0 = group-major, the default). */
+ * bits 11-13 = window flush block map (bit 11 chunk-major, bit 12 group rotated
+ * by row chunk; 0 = group-major, the default; bit 13 = records claimed
+ * dynamically by the LDS-DMA flush, block map ignored). */
 int spx_set_elim_variant(spx_ctx* ctx, int R, int target_wgs, int nt_flags, int interleave);
 /* The elimination variant in use: R, row chunks, column groups, nt flags,
  * interleave, pipelining, leading dimension. */
 int spx_get_elim_variant(const spx_ctx* ctx, int64_t out[7]);
-/* The window flush in use: variant and block map (bits 8-10 / 11-12 of
+/* The window flush in use: variant and block map (bits 8-10 / 11-13 of
  * spx_set_elim_variant's `interleave`), then the row chunks and column groups
  * of the last flush launch (0 before the first flush). */
 int spx_get_flush_variant(const spx_ctx* ctx, int64_t out[4]);

@@ -207,6 +207,7 @@ int free_buffers(spx_ctx* ctx) {
   dfree(ctx->win.epoch);
   dfree(ctx->win.nlist);
   dfree(ctx->win.rec);
+  dfree(ctx->win.claim);
   dfree(ctx->gr_enter);
   dfree(ctx->gr_ratio);
   ctx->loaded = false;
@@ -356,7 +357,7 @@ int flush_rch(const spx_ctx* ctx, int rt) {
   return (int)((ctx->m_local + rt * BLK - 1) / (rt * BLK));
 }
 // column groups: fill the resident capacity (blocks/CU x CUs) once, no tail wave
-int flush_groups(spx_ctx* ctx, const void* kern, int rch) {
+int flush_groups(spx_ctx* ctx, const void* kern, int rch, int threads = BLK) {
   if (ctx->tune_wgs > 0) return std::max(1, ctx->tune_wgs / rch);
   if (!ctx->n_cu) {
     (void)hipDeviceGetAttribute(&ctx->n_cu, hipDeviceAttributeMultiprocessorCount, ctx->device);
@@ -365,7 +366,7 @@ int flush_groups(spx_ctx* ctx, const void* kern, int rch) {
   int& bpc = ctx->flush_bpc[kern];
   if (!bpc) {
     int nb = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kern, BLK, 0) != hipSuccess || nb < 1)
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kern, threads, 0) != hipSuccess || nb < 1)
       nb = 2;
     bpc = nb;
   }
@@ -454,12 +455,12 @@ int enqueue_window_t(spx_ctx* ctx, int npiv, bool time_flush) {
     const int rc = record_event(ctx, e->first);
     if (rc) return rc;
   }
-  auto go = [&](auto kern, int rt) {
+  auto go = [&](auto kern, int rt, int threads = BLK) {
     const int rch = flush_rch(ctx, rt);
-    const int G = flush_groups(ctx, (const void*)kern, rch);
+    const int G = flush_groups(ctx, (const void*)kern, rch, threads);
     ctx->last_flush_G = G;
     ctx->last_flush_rch = rch;
-    hipLaunchKernelGGL(kern, dim3(rch * G), dim3(BLK), 0, ctx->stream, ctx->A, ctx->ld,
+    hipLaunchKernelGGL(kern, dim3(rch * G), dim3(threads), 0, ctx->stream, ctx->A, ctx->ld,
                        ctx->m_local, ctx->row0, ctx->N, ctx->win, npiv, rch, G, ctx->prm,
                        ctx->st, ctx->flush_map);
   };
@@ -479,6 +480,15 @@ int enqueue_window_t(spx_ctx* ctx, int npiv, bool time_flush) {
     case 6: nts ? go(flush_lds_kernel<KMAX, 9, true>, 2) : go(flush_lds_kernel<KMAX, 9, false>, 2); break;
     case 7: nts ? go(flush_lds_kernel<KMAX, 10, true>, 2) : go(flush_lds_kernel<KMAX, 10, false>, 2); break;
     default:
+      if (ctx->flush_map & 4) {  // records claimed dynamically (a claimer wave per block)
+        if (npiv < KMAX)
+          nts ? go(flush_dyn_kernel<KMAX, 12, true, true>, 2, BLK + 64)
+              : go(flush_dyn_kernel<KMAX, 12, false, true>, 2, BLK + 64);
+        else
+          nts ? go(flush_dyn_kernel<KMAX, 12, true>, 2, BLK + 64)
+              : go(flush_dyn_kernel<KMAX, 12, false>, 2, BLK + 64);
+        break;
+      }
       if (npiv < KMAX)  // the last window of a request: every slot guarded
         nts ? go(flush_lds_kernel<KMAX, 12, true, true>, 2) : go(flush_lds_kernel<KMAX, 12, false, true>, 2);
       else
@@ -641,13 +651,18 @@ int map_status(int32_t st) {
     case ST_UNBOUNDED: return SPX_UNBOUNDED;
     case ST_LIMIT: return SPX_ITER_LIMIT;
     case ST_FAULT: return SPX_E_STATE;
+    case ST_FLUSH_FAULT: return SPX_E_STATE;
     default: return SPX_RUNNING;
   }
 }
 
-// The device reported a fault (a persistent-chain exchange timed out).
+bool is_fault(int32_t st) { return st == ST_FAULT || st == ST_FLUSH_FAULT; }
+
+// The device reported a fault (an in-launch exchange timed out).
 int fault(spx_ctx* ctx) {
-  ctx->err = "device fault: a pivot-chain exchange timed out (blocks not co-resident?)";
+  ctx->err = ctx->h_st->status == ST_FLUSH_FAULT
+                 ? "device fault: a flush batch hand-off timed out"
+                 : "device fault: a pivot-chain exchange timed out (blocks not co-resident?)";
   return SPX_E_STATE;
 }
 
@@ -690,6 +705,9 @@ int alloc_common(spx_ctx* ctx, int64_t m_local, int64_t N, int64_t m_global, int
     HIPC(hipMemsetAsync(ctx->win.c, 0, sizeof(int64_t) * KW, ctx->stream));
     HIPC(hipMemsetAsync(ctx->win.tag, 0, sizeof(uint32_t) * N, ctx->stream));
     HIPC(hipMemsetAsync(ctx->win.epoch, 0, sizeof(uint32_t), ctx->stream));
+    ctx->win.nclaim = (int)std::max<int64_t>(1, (m_local + 2 * BLK - 1) / (2 * BLK));
+    HIPC(hipMalloc(&ctx->win.claim, sizeof(uint32_t) * ctx->win.nclaim));
+    HIPC(hipMemsetAsync(ctx->win.claim, 0, sizeof(uint32_t) * ctx->win.nclaim, ctx->stream));
     const size_t ge = sizeof(unsigned long long) * ENTER_REC * CHAIN_MAX_BLOCKS;
     const size_t gq = sizeof(unsigned long long) * RATIO_REC * CHAIN_MAX_BLOCKS;
     HIPC(hipMalloc(&ctx->gr_enter, ge));
@@ -1039,7 +1057,7 @@ int spx_solve(spx_ctx* ctx, const spx_opts* opts, spx_result* res) {
     }
   }
   if ((rc = pull_state(ctx))) return rc;  // the final state (after the extra chunk)
-  if (status < 0 || ctx->h_st->status == ST_FAULT) return fault(ctx);
+  if (status < 0 || is_fault(ctx->h_st->status)) return fault(ctx);
   double z = 0.0;
   HIPC(hipMemcpyAsync(&z, ctx->obj + (ctx->N - 1), sizeof(double), hipMemcpyDeviceToHost,
                       ctx->stream));
@@ -1084,7 +1102,7 @@ int spx_pivot_at(spx_ctx* ctx, int64_t r, int64_t c) {
   // pull the post-pivot state before writing the forced fields back
   if ((rc = pull_state(ctx))) return rc;
   const int32_t st_after = ctx->h_st->status;
-  if (st_after == ST_FAULT) return fault(ctx);
+  if (is_fault(st_after)) return fault(ctx);
   if ((rc = set_state_fields(ctx, st_after, -1, -1))) return rc;
   if ((rc = pull_state(ctx))) return rc;
   return st_after == ST_RUNNING ? SPX_OK : SPX_E_STATE;
@@ -1144,6 +1162,14 @@ int spx_run_pivots(spx_ctx* ctx, const spx_opts* opts, int64_t npivots, int time
 
 // Windowed (delayed) elimination: K pivots per tableau pass (2..16), 0/1 = off.
 #ifdef SPX_PHASE_TIMING
+// diagnostic build only: per-wave flush exit stamps (tools/probe_phases.py)
+int spx_probe_read_wave(unsigned long long* out, int n) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(spx::spx_probe_wave),
+                             sizeof(unsigned long long) * std::min(n, 2 * 4 * 8192)) ==
+                 hipSuccess
+             ? 0
+             : -1;
+}
 // diagnostic build only (tools/probe_phases.py): copy the phase timestamps
 int spx_probe_read(unsigned long long* out, int n) {
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(spx::spx_probe_buf),
@@ -1185,7 +1211,7 @@ int spx_state(spx_ctx* ctx, int32_t* status, int64_t* iters, double* objective) 
   CHECK_ARG(ctx->loaded, "no tableau loaded");
   int rc = pull_state(ctx);
   if (rc) return rc;
-  if (ctx->h_st->status == ST_FAULT) return fault(ctx);
+  if (is_fault(ctx->h_st->status)) return fault(ctx);
   if (status) *status = map_status(ctx->h_st->status);
   if (iters) *iters = ctx->h_st->iters;
   if (objective) {
@@ -1230,7 +1256,7 @@ int spx_set_elim_variant(spx_ctx* ctx, int R, int target_wgs, int nt_flags, int 
   ctx->elim_pipe = (interleave & 2) ? 0 : 1;  // bit 1 of `interleave`: disable pipelining
   ctx->elim_xcd = (interleave & 4) ? 1 : 0;   // bit 2: XCD-aware block swizzle
   ctx->flush_var = (interleave >> 8) & 7;     // bits 8-10: windowed flush variant
-  ctx->flush_map = (interleave >> 11) & 3;    // bits 11-12: flush block map
+  ctx->flush_map = (interleave >> 11) & 7;    // bits 11-13: flush block map (4: dynamic claims)
   choose_geometry(ctx);  // also resolves the automatic nt flags
   if (ctx->loaded) {
     if (ctx->rch > ctx->nbr) {  // ratio_part must hold rch partials

@@ -490,6 +490,7 @@ __global__ __launch_bounds__(CB) void chain_kernel(
         !load_extras<0>(gr_enter, wb, ENTER_HDR, q, 0, rec_tag(W, q - 1, GK_ENTER), pcl, unused,
                         st))
       return;
+    SPX_PROBE(q, 2, 0, fv != 12345.678 && pcl != 12345.678);  // loads arrived
     // RHS: apply slot q-1 (the slots before it are already in bcur)
     if (q > 0) bcur = apply_sel(bcur, i == r_prev, false, true, f_prev, prhs, skip);
 #pragma unroll
@@ -505,12 +506,12 @@ __global__ __launch_bounds__(CB) void chain_kernel(
         }
       }
     }
+    SPX_PROBE(q, 2, 1, fv != 12345.678);  // slots applied
 #pragma unroll
     for (int s = 0; s < KMAX; ++s) fs[s] = (s == q) ? fv : fs[s];
     f_prev = fv;
     KeyP k = keyp_none();
     if (ilive) {
-      win.F[(int64_t)q * ld + i] = fv;  // for the flush / row_fix (later kernels)
       if (forced_r >= 0) {
         if (i == forced_r) kmin2(k, 0.0, 0, i, 0.0, 0.0);
       } else if (fv > eps_piv) {
@@ -534,6 +535,9 @@ __global__ __launch_bounds__(CB) void chain_kernel(
       publish_record<NW, true>(gr_ratio, b, rec_tag(W, q, GK_RATIO), q + 1, sk, hl);
       SPX_PROBE_CHAIN(q, 0);
     }
+    // f_q for the flush / row_fix (later kernels): stored after the record, so
+    // these stores never queue in front of it
+    if (ilive) win.F[(int64_t)q * ld + i] = fv;
     SPX_PROBE(q, 0, 3, true);
     // ================= norm phase q =================
     SPX_PROBE(q, 1, 0, true);
@@ -566,6 +570,7 @@ __global__ __launch_bounds__(CB) void chain_kernel(
     if (!load_extras<1>(gr_ratio, wb, RATIO_HDR + 2, q + 1, RATIO_HDR, rec_tag(W, q, GK_RATIO),
                         frl, ex, st))
       return;
+    SPX_PROBE(q, 3, 0, v != 12345.678 && frl != 12345.678);  // loads arrived
     const double piv = rdlane(frl, q);
     prhs = ex[0] / piv;  // p_q[rhs]: lazy_norm's p = v / piv of the RHS column
     bool zb = false;
@@ -583,12 +588,14 @@ __global__ __launch_bounds__(CB) void chain_kernel(
         }
       }
     }
+    SPX_PROBE(q, 3, 1, v != 12345.678);  // slots applied
     KeyP ek = keyp_none();
+    double pq = 0.0;  // p_q[j]
     if (jlive) {
       const double p = v / piv;
+      pq = p;
 #pragma unroll
       for (int s = 0; s < KMAX; ++s) ps[s] = (s == q) ? p : ps[s];
-      win.P[j * KW + q] = p;  // for row_fix (a later kernel)
       const bool nz = (p != 0.0) || !skip;
       if (j == c) {
         o = 0.0;
@@ -611,20 +618,6 @@ __global__ __launch_bounds__(CB) void chain_kernel(
       slot_c = c;
     }
     r_prev = r;
-    if (leader) {
-      st->r = r;
-      st->c = c;
-      st->zc = zc;
-      st->piv = piv;
-      win.r[q] = r;
-      win.c[q] = c;
-      win.made[q] = 1;
-      basis[r] = c;
-      if (it < hist_cap) {
-        hist[2 * it] = r;
-        hist[2 * it + 1] = c;
-      }
-    }
     SPX_PROBE(q, 1, 2, v != 12345.678);
     ek = key_of_lane(ek, wave_argmin(ek.v, ek.t, ek.row >= 0, true));  // columns grow with the lane
     if (q + 1 < npiv && jlive && ek.row == j) {
@@ -646,6 +639,24 @@ __global__ __launch_bounds__(CB) void chain_kernel(
       }
       SPX_PROBE_CHAIN(q, 2);
     }
+    // stores for later kernels, after the record (never queued in front of it):
+    // p_q for row_fix, the pivot's bookkeeping
+    if (jlive) win.P[j * KW + q] = pq;
+    if (leader) {
+      st->r = r;
+      st->c = c;
+      st->zc = zc;
+      st->piv = piv;
+      win.r[q] = r;
+      win.c[q] = c;
+      win.made[q] = 1;
+      basis[r] = c;
+      if (it < hist_cap) {
+        hist[2 * it] = r;
+        hist[2 * it + 1] = c;
+      }
+    }
+
     SPX_PROBE(q, 1, 3, true);
   }
   // ---- the window ends after slot q (q pivots made) ----

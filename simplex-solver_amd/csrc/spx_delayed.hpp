@@ -49,12 +49,29 @@ __device__ unsigned long long spx_probe_buf[1024 + 2 * 8192];
       spx_probe_buf[(((slot) * 4 + (kind)) * 4 + (phase)) & 1023] =                          \
           __builtin_amdgcn_s_memrealtime();                                                  \
   } while (0)
+// flush waves: [2*(4*b + w)] = exit time, [.. + 1] = HW_ID | XCC_ID << 32 | columns << 40
+__device__ unsigned long long spx_probe_wave[2 * 4 * 8192];
+#define SPX_PROBE_WAVE(w, cols)                                                              \
+  do {                                                                                       \
+    if ((threadIdx.x & 63) == 0 && blockIdx.x < 8192) {                                      \
+      unsigned hw_, xc_;                                                                     \
+      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw_));                      \
+      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xc_));                     \
+      const int x_ = 2 * (4 * (int)blockIdx.x + (w));                                        \
+      spx_probe_wave[x_] = __builtin_amdgcn_s_memrealtime();                                 \
+      spx_probe_wave[x_ + 1] = (unsigned long long)hw_ | ((unsigned long long)(xc_ & 0xff) << 32) | \
+                               ((unsigned long long)(cols) << 40);                           \
+    }                                                                                        \
+  } while (0)
 #else
 #define SPX_PROBE(slot, kind, phase, cond) \
   do {                                     \
   } while (0)
 #define SPX_PROBE_BLOCK(which) \
   do {                         \
+  } while (0)
+#define SPX_PROBE_WAVE(w, cols) \
+  do {                          \
   } while (0)
 #endif
 
@@ -76,6 +93,9 @@ struct Window {
   int32_t* nlist;    // 1             : records in `rec` (reset by lazy_ratio slot 0)
   double* rec;       // N x RECW      : the window's touched columns, compacted by the
                      //                 last lazy_norm: [j | path flags, pad, p_0 .. p_{K-1}]
+  uint32_t* claim;   // nclaim        : flush_dyn_kernel's batch counter per row chunk
+                     //                 (zero between flushes: row_fix_kernel resets them)
+  int nclaim;
 };
 constexpr int RECW = KW + 2;  // doubles per record (272 B)
 
@@ -954,6 +974,264 @@ __global__ __launch_bounds__(BLK) void flush_lds_kernel(double* __restrict__ A, 
     hn = (k + D + 1 < cnt) ? hdr[rec_of(k + D + 1)] : 0;
   }
   wait_vmcnt<0>();  // no DMA may land in LDS after the wave has exited
+  SPX_PROBE_WAVE(w, cnt);
+  SPX_PROBE(K, 2, 1, true);
+  SPX_PROBE_BLOCK(1);
+}
+
+// ---------------------------------------------------------------------------
+// flush_dyn_kernel<K, D, NTS>: flush_lds_kernel's per-column update with the
+// records handed out dynamically, so every CU works until the list is done.
+//
+// Why: a CU runs 3 flush blocks, and the hardware issues the oldest wave
+// first, so with a static split (records g, g+G, ...) the CU's first block ends
+// ~45 us before its last, which then streams alone with a third of the bytes
+// in flight; CUs also end 16 us apart (profiles/r02/phases_flush_waves.log).
+//
+// How: the records are cut into batches of FB.  Batches 0 and 1 of block g are
+// static (records g*FB.., (G+g)*FB..); later ones are claimed from a per-row-
+// chunk counter (win.claim) with one returning atomic each.  A 5th wave per
+// block is the claimer: it keeps a mailbox of FMB batch bases in LDS ahead of
+// the 4 streaming waves, which read batch bases from LDS only.  So the
+// streaming waves' VMEM order stays exactly one LDS-DMA + one store per column
+// and the constant `s_waitcnt vmcnt` of flush_lds_kernel still retires exactly
+// the slot about to be read (an atomic issued by a streaming wave would join
+// that count).  The arithmetic per element is flush_lds_kernel's, operation for
+// operation; only which block updates a column changes, so the bytes are equal.
+// Every wait is bounded: a wave that waits ~1 s stores ST_FLUSH_FAULT and stops.
+// ---------------------------------------------------------------------------
+constexpr int FB = 8;    // records per batch
+constexpr int FMB = 8;   // mailbox entries (batch ordinals in flight per block)
+constexpr int32_t ST_FLUSH_FAULT = 6;
+constexpr unsigned FLUSH_SPIN_MAX = 1u << 23;
+// LDS words shared by the claimer and the streaming waves: relaxed
+// workgroup-scope atomics (plain ds_read / ds_write, no s_waitcnt of vmcnt;
+// a volatile access would make the compiler drain the wave's VMEM queue)
+__device__ __forceinline__ int lds_ld(int* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void lds_st(int* p, int v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+template <int K, int D, bool NTS, bool PART = false>
+__global__ __launch_bounds__(BLK + 64) void flush_dyn_kernel(double* __restrict__ A, int64_t ld,
+                                                             int64_t m_local, int64_t row0,
+                                                             int64_t N, Window win, int npiv,
+                                                             int rch, int G,
+                                                             const Params* __restrict__ prm,
+                                                             State* st, int fmap) {
+  static_assert(D >= 2 && D <= 16 && D + 1 < 2 * FB, "ring depth vs batch size");
+  __shared__ dbl2 ring[NWAVE * D * 64];
+  __shared__ int mbox[FMB];     // record base of batch ordinal n at [n % FMB]; -1: list done
+  __shared__ int produced;      // batch ordinals in the mailbox
+  __shared__ int procb[NWAVE];  // each streaming wave's current batch ordinal (process side)
+  SPX_PROBE(K, 2, 0, true);
+  SPX_PROBE_BLOCK(0);
+  int nm = 0;  // pivots made in this window: a prefix of its npiv slots
+  for (int s = 0; s < npiv; ++s) nm += win.made[s];
+  const int L = *win.nlist;
+  if (nm == 0) return;  // block-uniform
+  const bool full = nm == K;
+  const bool skip = prm->skip_zero != 0;
+  (void)fmap;
+  const int chunk = blockIdx.x % rch, g = blockIdx.x / rch;
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // 0..3 stream, 4 claims
+  if (threadIdx.x == 0) {
+    const int64_t b0 = (int64_t)g * FB, b1 = (int64_t)(G + g) * FB;
+    mbox[0] = b0 < L ? (int)b0 : -1;
+    mbox[1] = (b0 < L && b1 < L) ? (int)b1 : -1;
+    produced = 2;
+  }
+  if (threadIdx.x < NWAVE)
+    procb[threadIdx.x] =
+        (int64_t)chunk * 2 * BLK + (int64_t)threadIdx.x * 128 < m_local ? 0 : 0x7fffffff;
+  __syncthreads();
+  if (chunk == 0 && g == 0 && threadIdx.x == 0) {
+    atomicAdd(reinterpret_cast<unsigned long long*>(&st->touched_total), (unsigned long long)L);
+    st->iters += nm;
+  }
+  if (w == NWAVE) {
+    // ---- the claimer: one lane; batch ordinals 2, 3, ... while there is room ----
+    if (lane != 0 || lds_ld(&mbox[1]) < 0) {
+      if (lane == 0) {  // static batches already end the list
+        lds_st(&mbox[2 % FMB], -1);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the entry before the count
+        lds_st(&produced, 3);
+      }
+      return;
+    }
+    unsigned spins = 0;
+    for (int n = 2;;) {
+      int minp = lds_ld(&procb[0]);
+#pragma unroll
+      for (int x = 1; x < NWAVE; ++x) minp = min(minp, lds_ld(&procb[x]));
+      // room: the slowest streaming wave no longer reads slot n % FMB (finished
+      // or inactive waves hold 0x7fffffff)
+      if (minp < 0x7fffffff - FMB && n >= minp + FMB) {
+        if (++spins > FLUSH_SPIN_MAX) {
+          st->status = ST_FLUSH_FAULT;
+          lds_st(&mbox[n % FMB], -1);
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          lds_st(&produced, n + 1);
+          return;
+        }
+        __builtin_amdgcn_s_sleep(2);
+        continue;
+      }
+      const unsigned t = __hip_atomic_fetch_add(win.claim + chunk, 1u, __ATOMIC_RELAXED,
+                                                __HIP_MEMORY_SCOPE_AGENT);
+      const int64_t b = (int64_t)(2 * G + (int64_t)t) * FB;
+      const int base = b < L ? (int)b : -1;
+      lds_st(&mbox[n % FMB], base);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      lds_st(&produced, n + 1);
+      ++n;
+      if (base < 0) return;
+    }
+  }
+  // ---- streaming waves ----
+  const int64_t wrow = (int64_t)chunk * 2 * BLK + (int64_t)w * 128;  // this wave's first row
+  if (wrow >= m_local) return;  // wave-uniform (procb already says "never blocks the claimer")
+  const int64_t i0 = wrow + 2 * lane;
+  const bool ok = i0 < m_local;            // the pair (i0, i0+1) holds local rows
+  const int64_t i0c = ok ? i0 : wrow;      // in-column address for idle lanes
+  double f[K][2];
+#pragma unroll
+  for (int s = 0; s < K; ++s) {
+    dbl2 fv = dbl2{0.0, 0.0};
+    if (s < nm && ok) fv = ld2<false>(win.F + (int64_t)s * ld + i0);
+    f[s][0] = fv.x;
+    f[s][1] = fv.y;
+  }
+  typedef const __attribute__((address_space(4))) double cdbl;
+  typedef const __attribute__((address_space(4))) int64_t ci64;
+  cdbl* rec = (cdbl*)win.rec;
+  ci64* hdr = (ci64*)win.rec;
+  ci64* wr = (ci64*)win.r;
+  ci64* wc = (ci64*)win.c;
+  const uint32_t lds0 =
+      (uint32_t)(uintptr_t)((__attribute__((address_space(3))) dbl2*)&ring[0]) +
+      (uint32_t)(w * D * 64) * (uint32_t)sizeof(dbl2);
+  bool fault = false;
+  // batch ordinal n's record base (the claimer may still be on it: bounded wait)
+  auto batch = [&](int n) -> int {
+    unsigned spins = 0;
+    while (__builtin_amdgcn_readfirstlane(lds_ld(&produced)) <= n) {
+      if (++spins > FLUSH_SPIN_MAX) {
+        fault = true;
+        return -1;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+    asm volatile("" ::: "memory");  // the entry is read after the count
+    return __builtin_amdgcn_readfirstlane(lds_ld(&mbox[n % FMB]));
+  };
+  auto blen = [&](int base) -> int { return base < 0 ? 0 : min(FB, L - base); };
+  // issue cursor (LDS-DMA side, D + 1 columns ahead) and process cursor
+  int ni = 0, ib = batch(0), io = 0, il = blen(ib);
+  auto issue_next = [&]() -> int {  // record index at the issue cursor (then advance); -1: done
+    if (ib < 0) return -1;
+    const int r = ib + io;
+    if (++io == il) {
+      ib = batch(++ni);
+      io = 0;
+      il = blen(ib);
+    }
+    return r;
+  };
+  int np = 0, pb = ib, po = 0, pl = il;
+  auto proc_next = [&]() -> int {  // advance the process cursor; its record index or -1
+    if (++po == pl) {
+      ++np;
+      if (lane == 0) lds_st(&procb[w], np);  // ordinals < np are free for the claimer
+      asm volatile("" ::: "memory");
+      pb = __builtin_amdgcn_readfirstlane(lds_ld(&mbox[np % FMB]));  // the issue side passed it
+      po = 0;
+      pl = blen(pb);
+    }
+    return pb < 0 ? -1 : pb + po;
+  };
+  const int r0 = issue_next();
+  if (r0 < 0) {
+    if (lane == 0) lds_st(&procb[w], 0x7fffffff);
+    if (fault) st->status = ST_FLUSH_FAULT;
+    return;
+  }
+#pragma unroll
+  for (int s = 0; s < K; ++s) asm volatile("" ::"v"(f[s][0]), "v"(f[s][1]));
+  wait_vmcnt<0>();
+  // prologue: columns 0..D-1 (dummy re-reads of the last real column past the end)
+  const double* last_src = A + (hdr[(int64_t)r0 * RECW] & 0xffffffffll) * ld + i0c;
+  glds16(last_src, lds0);
+#pragma unroll
+  for (int d = 1; d < D; ++d) {
+    const int rd = issue_next();
+    if (rd >= 0) last_src = A + (hdr[(int64_t)rd * RECW] & 0xffffffffll) * ld + i0c;
+    glds16(last_src, lds0 + (uint32_t)(d * 64 * sizeof(dbl2)));
+  }
+  int rn = issue_next();                                  // column D (next DMA)
+  int64_t hn = rn >= 0 ? hdr[(int64_t)rn * RECW] : 0;
+  int64_t hc = hdr[(int64_t)r0 * RECW];                   // the column being updated
+  double pc[K];
+#pragma unroll
+  for (int s = 0; s < K; ++s) pc[s] = rec[(int64_t)r0 * RECW + 2 + s];
+  int cols = 0;
+  for (int k = 0;; ++k) {
+    const int slot = k % D;
+    if (k >= D - 1) wait_vmcnt<2 * (D - 1)>();
+    else wait_vmcnt<D - 1>();
+    dbl2 x = ring[(w * D + slot) * 64 + lane];
+    const int64_t j = hc & 0xffffffffll;
+    if ((hc >> 32) == 0 && (PART || full)) {
+      if constexpr (!PART) {
+#pragma unroll
+        for (int s = 0; s < K; ++s) {
+          x.x = msub(x.x, f[s][0], pc[s]);
+          x.y = msub(x.y, f[s][1], pc[s]);
+        }
+      } else {
+#pragma unroll
+        for (int s = 0; s < K; ++s) {
+          if (s < nm) {
+            x.x = msub(x.x, f[s][0], pc[s]);
+            x.y = msub(x.y, f[s][1], pc[s]);
+          }
+        }
+      }
+    } else {
+      ci64* wrk = wr;
+      ci64* wck = wc;
+      asm volatile("" : "+s"(wrk), "+s"(wck));
+#pragma unroll
+      for (int s = 0; s < K; ++s) {
+        if (s < nm) {
+          const int64_t rl = wrk[s] - row0;
+          const int64_t cs = wck[s];
+          x.x = apply_pivot(x.x, i0, j, rl, cs, f[s][0], pc[s], skip);
+          x.y = apply_pivot(x.y, i0 + 1, j, rl, cs, f[s][1], pc[s], skip);
+        }
+      }
+    }
+    if (ok) st2<NTS>(A + j * ld + i0, x);
+    ++cols;
+    // DMA of column k + D into the slot just read (a dummy re-read past the end)
+    if (rn >= 0) last_src = A + (hn & 0xffffffffll) * ld + i0c;
+    glds16(last_src, lds0 + (uint32_t)(slot * 64 * sizeof(dbl2)));
+    const int rk = proc_next();  // column k + 1
+    if (rk < 0) break;
+    hc = hdr[(int64_t)rk * RECW];
+#pragma unroll
+    for (int s = 0; s < K; ++s) pc[s] = rec[(int64_t)rk * RECW + 2 + s];
+    rn = issue_next();  // column k + D + 1
+    hn = rn >= 0 ? hdr[(int64_t)rn * RECW] : 0;
+  }
+  wait_vmcnt<0>();  // no DMA may land in LDS after the wave has exited
+  if (lane == 0) lds_st(&procb[w], 0x7fffffff);
+  if (fault) st->status = ST_FLUSH_FAULT;
+  SPX_PROBE_WAVE(w, cols);
+  (void)cols;
   SPX_PROBE(K, 2, 1, true);
   SPX_PROBE_BLOCK(1);
 }
@@ -972,6 +1250,10 @@ __global__ __launch_bounds__(BLK) void row_fix_kernel(double* __restrict__ A, in
   __shared__ double fr[K][K];  // fr[L][s] = f_s[r_L]
   __shared__ int64_t rows[K];
   __shared__ int lastL[K];
+  // the flush's batch counters start at zero for the next window (this kernel
+  // follows every flush on the stream)
+  if (blockIdx.x == 0)
+    for (int t = threadIdx.x; t < win.nclaim; t += BLK) win.claim[t] = 0u;
   // all loads are independent: issue them together
   const int64_t j = (int64_t)blockIdx.x * BLK + threadIdx.x;
   const bool live = j < N;

@@ -328,8 +328,9 @@ class DeviceTableau:
         `interleave` word packs: bit 0 interleaved columns, bit 1 pipelining
         OFF, bit 2 XCD-aware swizzle, bits 8-10 window flush variant (0 the
         LDS-DMA ring of 12, 6/7 rings of 9/10, 1-5 register rings for
-        power-of-two K), bits 11-12 flush block map (bit 11 chunk-major, bit 12
-        groups rotated by row chunk).  Pass `interleave` to set the whole word,
+        power-of-two K), bits 11-13 flush block map (bit 11 chunk-major, bit 12
+        groups rotated by row chunk; 4 = bit 13: the LDS-DMA flush claims its
+        columns dynamically, block map ignored).  Pass `interleave` to set the whole word,
         or leave it None and give only the keyword fields to change: the others
         keep their current values (read back with elim_variant())."""
         if interleave is None:
@@ -339,7 +340,7 @@ class DeviceTableau:
             fv = v["flush_var"] if flush_variant is None else int(flush_variant)
             fm = v["flush_map"] if flush_map is None else int(flush_map)
             interleave = (v["interleave"] & 1) | (0 if pipe else 2) | (4 if xc else 0)
-            interleave |= (fv & 7) << 8 | (fm & 3) << 11
+            interleave |= (fv & 7) << 8 | (fm & 7) << 11
         self._check(self._lib.spx_set_elim_variant(self._ctx, int(R), int(target_wgs),
                                                    int(nt_flags), int(interleave)),
                     "spx_set_elim_variant")

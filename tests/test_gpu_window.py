@@ -64,7 +64,7 @@ def _set_flush_variant(e, fv):
     assert (v["flush_var"], v["flush_map"]) == (fv & 7, fv >> 3)
 
 
-@pytest.mark.parametrize("fv", list(range(8)) + [8, 16, 24, 14])
+@pytest.mark.parametrize("fv", list(range(8)) + [8, 16, 24, 14, 32, 33])
 @pytest.mark.parametrize("K", [2, 12, 16, 24, 32])
 @pytest.mark.parametrize("shape", [(17, 40), (700, 1500), (1537, 2600)])
 def test_window_flush_variants_bit_exact(eng_cls, fv, K, shape):

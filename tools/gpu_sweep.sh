@@ -1,0 +1,27 @@
+#!/bin/bash
+# A/B sweep of bench.py configurations, interleaved over ROUNDS rounds, one
+# bench process per configuration.  CONFIGS: ';'-separated bench argument
+# lists.  Output: gpurun_out/$OUT/sweep.jsonl (value + flush time per run).
+set -u
+cd "${GRAFT_REPO_ROOT}"
+export TMPDIR=/tmp
+O=gpurun_out/${OUT:-sweep}
+mkdir -p "$O"
+IFS=';' read -ra CF <<< "${CONFIGS}"
+for r in $(seq 1 "${ROUNDS:-2}"); do
+  for c in "${CF[@]}"; do
+    timeout -k 10 200 python bench.py --cpu-seconds 0 ${STEPS:---steps 40 --warmup 5} $c > "$O/last.log" 2>&1
+    rc=$?
+    if [ $rc != 0 ]; then echo "config [$c] rc=$rc"; tail -5 "$O/last.log"; exit $rc; fi
+    python - "$c" "$r" "$O/last.log" >> "$O/sweep.jsonl" <<'EOF'
+import json, sys
+d = json.loads([l for l in open(sys.argv[3]) if l.startswith("{")][-1])
+print(json.dumps({"args": sys.argv[1], "round": int(sys.argv[2]), "value": round(d["value"], 1),
+                  "ms_per_step": round(d["ms_per_step"], 4), "flush_us": round(d["roofline"]["avg_launch_us"], 1),
+                  "frac": round(d["roofline"]["frac"], 4), "chain_blocks": d["config"].get("chain_blocks"),
+                  "groups": d["config"]["elim_variant"].get("flush_groups")}))
+EOF
+    tail -1 "$O/sweep.jsonl"
+  done
+done
+exit 0

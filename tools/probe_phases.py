@@ -74,6 +74,10 @@ def main():
                   f"  phase1 +{ph[1]-ph[0]:5.2f}  phase2 +{ph[2]-ph[1]:5.2f}"
                   f"  end +{ph[3]-ph[2]:5.2f}  total {ph[3]-ph[0]:5.2f}")
             prev_end = ph[3]
+            if not a.chain and t(q, 2 + kind, 0) > t0:
+                a0, a1 = us(t(q, 2 + kind, 0)), us(t(q, 2 + kind, 1))
+                print(f"       fine: loads arrived +{a0 - ph[1]:5.2f}  slots applied "
+                      f"+{a1 - a0:5.2f}  rest of phase2 +{ph[2] - a1:5.2f}")
             if kind == 0 and os.environ.get("SPX_PROBE_FINE"):
                 k0, k1 = us(t(q, 2, 0)), us(t(q, 2, 1))
                 print(f"       fine: keys reduced +{k0 - ph[0]:5.2f}  wave_min +{k1 - k0:5.2f}")
@@ -118,6 +122,36 @@ def main():
     print("  per-chunk mean dur:", " ".join(f"{x:.0f}" for x in cd))
     xcd = np.arange(nblk) % 8
     print("  per-XCD mean dur:", " ".join(f"{dur[xcd == k].mean():.0f}" for k in range(8)))
+    if hasattr(lib, "spx_probe_read_wave"):
+        wb = (ctypes.c_ulonglong * (2 * 4 * 8192))()
+        assert lib.spx_probe_read_wave(wb, 2 * 4 * 8192) == 0
+        raw = np.frombuffer(wb, dtype=np.uint64).reshape(8192, 4, 2)[:nblk]
+        wend = (raw[:, :, 0].astype(np.float64) - t0) / 100.0 - f0  # us from flush entry
+        info = raw[:, :, 1]
+        live = raw[:, :, 0] > 0
+        hw = (info & np.uint64(0xffffffff)).astype(np.int64)
+        xc = ((info >> np.uint64(32)) & np.uint64(0xff)).astype(np.int64)
+        cols = (info >> np.uint64(40)).astype(np.int64)
+        cu = (xc << 16) | ((hw >> 8) & 0xff)  # XCC, SE/SH/CU bits of HW_ID
+        wdur = wend - st[:, None]
+        print(f"  waves: {live.sum()} live; end pct 0/10/50/90/100: {q(wend[live])}")
+        print("  per-wave-index mean end:", " ".join(f"{wend[:, w][live[:, w]].mean():.1f}"
+                                                     for w in range(4)))
+        ucu = np.unique(cu[live])
+        cu_end = np.array([wend[live & (cu == c)].max() for c in ucu])
+        cu_nb = np.array([len(np.unique(np.nonzero(live & (cu == c))[0])) for c in ucu])
+        print(f"  CUs {len(ucu)}; blocks per CU {np.bincount(cu_nb)}; per-CU last wave end "
+              f"pct 0/10/50/90/100: {q(cu_end)}")
+        us_per_col = wdur[live] / np.maximum(cols[live], 1)
+        print(f"  us per column per wave pct 0/10/50/90/100: {q(us_per_col)}")
+        gmean = np.array([wdur[(g == k)[:, None] & live].mean() for k in range(G.value)])
+        order = np.argsort(gmean)
+        print("  fastest groups:", " ".join(f"{k}:{gmean[k]:.0f}" for k in order[:8]))
+        print("  slowest groups:", " ".join(f"{k}:{gmean[k]:.0f}" for k in order[-8:]))
+        out = os.environ.get("PROBE_NPZ")
+        if out:
+            np.savez(out, st=st, en=en, wend=wend, hw=hw, xc=xc, cols=cols, live=live,
+                     rch=rch.value, G=G.value)
     e.close()
 
 
