@@ -1,7 +1,9 @@
 #!/bin/bash
 # A/B sweep of bench.py configurations, interleaved over ROUNDS rounds, one
 # bench process per configuration.  CONFIGS: ';'-separated bench argument
-# lists.  Output: gpurun_out/$OUT/sweep.jsonl (value + flush time per run).
+# lists, each optionally prefixed "NAME|" to run with
+# simplex_amd/lib/libspx_NAME.so (same-box A/B of two builds).  Output:
+# gpurun_out/$OUT/sweep.jsonl (value + flush time per run).
 set -u
 cd "${GRAFT_REPO_ROOT}"
 export TMPDIR=/tmp
@@ -9,11 +11,14 @@ O=gpurun_out/${OUT:-sweep}
 mkdir -p "$O"
 IFS=';' read -ra CF <<< "${CONFIGS}"
 for r in $(seq 1 "${ROUNDS:-2}"); do
-  for c in "${CF[@]}"; do
+  for cfg in "${CF[@]}"; do
+    lib=""; c="$cfg"
+    if [[ "$cfg" == *"|"* ]]; then lib="${cfg%%|*}"; c="${cfg#*|}"; fi
+    if [ -n "$lib" ]; then export SPX_LIB="$PWD/simplex-solver_amd/simplex_amd/lib/libspx_$lib.so"; else unset SPX_LIB; fi
     timeout -k 10 200 python bench.py --cpu-seconds 0 ${STEPS:---steps 40 --warmup 5} $c > "$O/last.log" 2>&1
     rc=$?
     if [ $rc != 0 ]; then echo "config [$c] rc=$rc"; tail -5 "$O/last.log"; exit $rc; fi
-    python - "$c" "$r" "$O/last.log" >> "$O/sweep.jsonl" <<'EOF'
+    python - "$cfg" "$r" "$O/last.log" >> "$O/sweep.jsonl" <<'EOF'
 import json, sys
 d = json.loads([l for l in open(sys.argv[3]) if l.startswith("{")][-1])
 print(json.dumps({"args": sys.argv[1], "round": int(sys.argv[2]), "value": round(d["value"], 1),
