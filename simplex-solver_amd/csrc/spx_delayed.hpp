@@ -914,8 +914,20 @@ __global__ __launch_bounds__(BLK) void flush_lds_kernel(double* __restrict__ A, 
   double pc[K];
 #pragma unroll
   for (int s = 0; s < K; ++s) pc[s] = rec[rec_of(0) + 2 + s];
+  const int pq1 = cnt >> 2, pq2 = cnt >> 1, pq3 = cnt - (cnt >> 2);  // quarters of the work
   for (int k = 0; k < cnt; ++k) {
     const int slot = k % D;
+    if ((k & 7) == 0) {
+      // issue priority by work left: a wave ahead of its CU's others yields
+      // issue slots to them (the hardware otherwise prefers the oldest wave,
+      // so a CU's first-dispatched block ended ~45 us before its last, which
+      // then streamed alone; profiles/r02/phases_flush_waves.log)
+      const int rem = cnt - k;
+      if (rem > pq3) __builtin_amdgcn_s_setprio(3);
+      else if (rem > pq2) __builtin_amdgcn_s_setprio(2);
+      else if (rem > pq1) __builtin_amdgcn_s_setprio(1);
+      else __builtin_amdgcn_s_setprio(0);
+    }
     // retire column k's DMA: 2 VMEM ops per later column, fewer in the prologue
     if (k >= D - 1) wait_vmcnt<2 * (D - 1)>();
     else wait_vmcnt<D - 1>();
