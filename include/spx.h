@@ -188,10 +188,9 @@ int spx_get_flush_variant(const spx_ctx* ctx, int64_t out[4]);
 int spx_set_window(spx_ctx* ctx, int K);
 /* Pivot chain of a window (the K pivot choices before its flush): mode 0
  * (default) runs them as ONE persistent launch when the tableau fits (at most
- * 512 x CUs columns and rows, single-GPU contexts; DESIGN.md §4b), mode 1 as two
+ * 512 x CUs columns and rows, single-GPU contexts; DESIGN.md §4c), mode 1 as two
  * launches per pivot, modes 2 / 3 force the persistent chain's 256- / 512-thread
- * blocks, mode 4 runs it with a communication wave per block that posts
- * speculative exchange winners.  Results are bit-identical.  min_blocks (0..256) raises the
+ * blocks.  Results are bit-identical.  min_blocks (0..256) raises the
  * persistent grid above its minimum (tuning; 0 = minimum). */
 int spx_set_chain(spx_ctx* ctx, int mode, int min_blocks);
 /* Blocks of the persistent chain the loaded tableau uses (0: not used). */

@@ -390,9 +390,7 @@ int chain_blocks(spx_ctx* ctx, int* cb_out = nullptr) {
     if (ctx->n_cu <= 0) ctx->n_cu = 256;
   }
   const int64_t wide = std::max<int64_t>(ctx->N, ctx->m_local);
-  // mode 4: 192 compute threads + the communication wave = 256 threads, one
-  // wave per SIMD (a 5th wave would halve the VGPR budget: 135 VGPRs spilled)
-  const int cb = ctx->chain_mode == 4 ? 192 : ctx->chain_mode == 2 ? 256 : ctx->chain_mode == 3 ? 512
+  const int cb = ctx->chain_mode == 2 ? 256 : ctx->chain_mode == 3 ? 512
                  : (wide > 256 * std::min(ctx->n_cu, CHAIN_MAX_BLOCKS) ? 512 : 256);
   if (cb_out) *cb_out = cb;
   const int64_t need = std::max<int64_t>({(ctx->N + cb - 1) / cb, (ctx->m_local + cb - 1) / cb,
@@ -409,13 +407,8 @@ int enqueue_window_t(spx_ctx* ctx, int npiv, bool time_flush) {
   if (B > 0) {
     const int cpb = (int)((ctx->N + B - 1) / B);
     const int rpb = (int)((ctx->m_local + B - 1) / B);
-    // mode 4: 192 compute threads + a communication wave that posts
-    // speculative exchange winners (spx_chain.hpp, "Speculative hand-off")
-    const bool spec = ctx->chain_mode == 4;
-    auto kern = spec ? chain_kernel<KMAX, 192, true>
-                : cb == 512 ? chain_kernel<KMAX, 512> : chain_kernel<KMAX, 256>;
-    hipLaunchKernelGGL(kern, dim3(B), dim3(spec ? cb + 64 : cb), 0, ctx->stream, ctx->enter_part,
-                       ctx->st,
+    auto kern = cb == 512 ? chain_kernel<KMAX, 512> : chain_kernel<KMAX, 256>;
+    hipLaunchKernelGGL(kern, dim3(B), dim3(cb), 0, ctx->stream, ctx->enter_part, ctx->st,
                        (const Params*)ctx->prm, std::max(NWAVE * ctx->nbn, B),
                        (const double*)ctx->A, ctx->ld, ctx->m_local, ctx->N, ctx->obj, ctx->win,
                        npiv, ctx->basis, ctx->hist, ctx->gr_enter, ctx->gr_ratio, cpb, rpb);
@@ -1324,13 +1317,12 @@ int spx_get_elim_variant(const spx_ctx* ctx, int64_t out[7]) {
 // Pivot chain of a window: mode 0 = one persistent launch per window when the
 // tableau fits (<= 512 x CUs columns and rows; single-GPU contexts), 1 = two
 // launches per pivot (lazy_ratio -> lazy_norm), 2 / 3 = the persistent chain
-// with 256- / 512-thread blocks, 4 = the persistent chain with speculative
-// exchange posts (192 compute threads + 64).  min_blocks raises the persistent grid above
+// with 256- / 512-thread blocks.  min_blocks raises the persistent grid above
 // its minimum (tuning; 0 = minimum).
 int spx_set_chain(spx_ctx* ctx, int mode, int min_blocks) {
   if (!ctx) return SPX_E_ARG;
-  CHECK_ARG(mode >= 0 && mode <= 4 && min_blocks >= 0 && min_blocks <= CHAIN_MAX_BLOCKS,
-            "chain mode must be 0..4, min_blocks 0..256");
+  CHECK_ARG(mode >= 0 && mode <= 3 && min_blocks >= 0 && min_blocks <= CHAIN_MAX_BLOCKS,
+            "chain mode must be 0..3, min_blocks 0..256");
   ctx->chain_mode = mode;
   ctx->chain_min_blocks = min_blocks;
   drop_graphs(ctx);

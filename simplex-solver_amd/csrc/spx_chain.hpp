@@ -51,7 +51,7 @@ namespace spx {
 __device__ unsigned long long spx_probe_chain[32 * 4 * 256];
 #define SPX_PROBE_CHAIN(q, ev)                                                            \
   do {                                                                                   \
-    if ((threadIdx.x & 63) == 0 && blockIdx.x < 256 && (q) < 32)                         \
+    if (threadIdx.x == 0 && blockIdx.x < 256 && (q) < 32)                                \
       spx_probe_chain[((q) * 4 + (ev)) * 256 + blockIdx.x] = __builtin_amdgcn_s_memrealtime(); \
   } while (0)
 #else
@@ -358,172 +358,6 @@ __device__ __forceinline__ void publish_record(gu64* rec, int b, unsigned tag, i
 }
 
 // ---------------------------------------------------------------------------
-// Speculative hand-off inside a block (chain mode 4).  A dedicated
-// communication wave polls the record headers; after every pass that is not
-// yet complete it posts the best record among those fully arrived, and the
-// final winner once every tag matched.  A post is {index, block, value} in LDS
-// plus a control word (phase id << 8 | final << 7 | version), written after
-// the payload.  The compute waves spin on the control word and, for every new
-// post, issue the phase's dependent loads (the stale tableau value and one
-// pass over the posted record's history granules) at once, so a winner that
-// published early has its loads in flight before the last block publishes.
-// Only the final post is acted on; its history is re-validated by tag.
-// ---------------------------------------------------------------------------
-struct SpecBox {
-  int64_t idx;
-  double val;
-  int blk;
-  int ctl;
-};
-__device__ __forceinline__ int lds_ld_i(int* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-__device__ __forceinline__ void lds_st_i(int* p, int v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-// comm wave, lane 0: post (idx, blk, val) as version `ver` of phase `pid`
-__device__ __forceinline__ void spec_post(SpecBox* sb, int pid, int ver, bool fin, int64_t idx,
-                                          int blk, double val) {
-  sb->idx = idx;
-  sb->blk = blk;
-  sb->val = val;
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the payload before the control word
-  lds_st_i(&sb->ctl, (pid << 8) | (fin ? 0x80 : 0) | (ver & 0x7f));
-}
-
-// The comm wave's poll: poll_records_n plus a post of the best fully-arrived
-// record after every incomplete pass (when it changed) and of the winner.
-template <bool RATIO, int G, int RPL>
-__device__ __forceinline__ bool poll_records_spec(const gu64* recs, int B, unsigned tag, int rule,
-                                                  KeyP& k, State* st, SpecBox* sb, int pid) {
-  const int lane = threadIdx.x & 63;
-  const bool mono = RPL == 1 && !(RATIO && rule == RULE_BLAND);
-  int ver = 0;
-  int64_t posted = -3;
-  int posted_b = -1;
-  for (unsigned spins = 0;;) {
-    unsigned long long g[RPL][4];
-#pragma unroll
-    for (int x = 0; x < RPL; ++x) {
-      const int b = min(lane + 64 * x, B - 1);
-#pragma unroll
-      for (int u = 0; u < 4; ++u)
-        g[x][u] = u < G ? g_load(recs + (size_t)u * CHAIN_MAX_BLOCKS + b)
-                        : (unsigned long long)tag << 32;
-    }
-    bool okx[RPL];
-    bool ok = true;
-#pragma unroll
-    for (int x = 0; x < RPL; ++x) {
-      okx[x] = true;
-#pragma unroll
-      for (int u = 0; u < 4; ++u) okx[x] &= (unsigned)(g[x][u] >> 32) == tag;
-      ok &= okx[x];
-    }
-    const bool done = __all(ok);
-    k = keyp_none();
-#pragma unroll
-    for (int x = 0; x < RPL; ++x)
-      if (lane + 64 * x < B && okx[x]) decode_record<RATIO>(k, g[x], lane + 64 * x, rule);
-    KeyP w = key_of_lane(k, wave_argmin(k.v, k.t, k.row >= 0, mono));
-    if (done) {
-      k = w;
-      if (lane == 0) spec_post(sb, pid, ++ver, true, k.row, (int)k.b, k.a);
-      break;
-    }
-    if (w.row >= 0 && (w.row != posted || (int)w.b != posted_b)) {
-      posted = w.row;
-      posted_b = (int)w.b;
-      if (lane == 0) spec_post(sb, pid, ++ver, false, w.row, (int)w.b, w.a);
-    }
-    if (spin_fail(spins, st)) {
-      if (lane == 0) spec_post(sb, pid, ++ver, true, -2, 0, 0.0);
-      return false;
-    }
-  }
-  asm volatile("" ::: "memory");
-  return true;
-}
-template <bool RATIO, int G>
-__device__ __forceinline__ bool poll_spec(const gu64* recs, int B, unsigned tag, int rule, KeyP& k,
-                                          State* st, SpecBox* sb, int pid) {
-  if (B <= 64) return poll_records_spec<RATIO, G, 1>(recs, B, tag, rule, k, st, sb, pid);
-  if (B <= 128) return poll_records_spec<RATIO, G, 2>(recs, B, tag, rule, k, st, sb, pid);
-  return poll_records_spec<RATIO, G, 4>(recs, B, tag, rule, k, st, sb, pid);
-}
-
-// One pass of load_extras' loads (no wait on the tags): raw granules.
-template <int NE>
-struct ExRaw {
-  unsigned long long lo, hi, x[2 * NE > 0 ? 2 * NE : 1];
-};
-template <int NE>
-__device__ __forceinline__ void extras_issue(ExRaw<NE>& e, const gu64* rec, int wb, int h0, int n,
-                                             int e0) {
-  const int lane = threadIdx.x & 63;
-  const bool mine = lane < n;
-  const gu64* g = rec + (size_t)(h0 + 2 * (mine ? lane : 0)) * CHAIN_MAX_BLOCKS + wb;
-  const gu64* x = rec + (size_t)e0 * CHAIN_MAX_BLOCKS + wb;
-  e.lo = g_load(g);
-  e.hi = g_load(g + CHAIN_MAX_BLOCKS);
-#pragma unroll
-  for (int u = 0; u < 2 * NE; ++u) e.x[u] = g_load(x + (size_t)u * CHAIN_MAX_BLOCKS);
-}
-template <int NE>
-__device__ __forceinline__ bool extras_ok(const ExRaw<NE>& e, int n, unsigned tag, double& hv,
-                                          double (&ev)[2]) {
-  const bool mine = (threadIdx.x & 63) < n;
-  bool good = !mine || ((unsigned)(e.lo >> 32) == tag && (unsigned)(e.hi >> 32) == tag);
-#pragma unroll
-  for (int u = 0; u < 2 * NE; ++u) good &= (unsigned)(e.x[u] >> 32) == tag;
-  if (!__all(good)) return false;
-  hv = mine ? g_decode_d(e.lo, e.hi) : 0.0;
-#pragma unroll
-  for (int u = 0; u < NE; ++u) ev[u] = g_decode_d(e.x[2 * u], e.x[2 * u + 1]);
-  return true;
-}
-
-// Compute waves: wait for the final post of phase `pid`; for every new posted
-// winner issue the stale value at `gaddr(idx)` and one pass of its record's
-// history.  Returns the final (idx, blk, val) and the value / raw history
-// loaded for it (reloaded if the final winner was never posted before).
-template <int NE, typename Addr>
-__device__ __forceinline__ void spec_wait(SpecBox* sb, int pid, State* st, Addr gaddr,
-                                          const gu64* rec, int h0, int n, int e0, int64_t& idx,
-                                          int& blk, double& val, double& gv, ExRaw<NE>& ex) {
-  int seen = -1;
-  idx = -3;
-  blk = -1;
-  for (unsigned spins = 0;;) {
-    const int ctl = __builtin_amdgcn_readfirstlane(lds_ld_i(&sb->ctl));
-    if ((ctl >> 8) == pid) {
-      const int ver = ctl & 0x7f;
-      if (ver != seen) {
-        seen = ver;
-        asm volatile("" ::: "memory");  // the payload is read after the control word
-        const int64_t ni = __builtin_amdgcn_readfirstlane((int)sb->idx) |
-                           ((int64_t)__builtin_amdgcn_readfirstlane((int)(sb->idx >> 32)) << 32);
-        const int nb = __builtin_amdgcn_readfirstlane(sb->blk);
-        const double nv = sb->val;
-        if (ni >= 0 && (ni != idx || nb != blk)) {
-          gv = *gaddr(ni);
-          extras_issue<NE>(ex, rec, nb, h0, n, e0);
-        }
-        idx = ni;
-        blk = nb;
-        val = nv;
-      }
-      if (ctl & 0x80) return;
-    }
-    if (++spins > CHAIN_SPIN_MAX) {  // the comm wave itself gives up first
-      idx = -2;
-      return;
-    }
-    __builtin_amdgcn_s_sleep(1);
-  }
-}
-
-// ---------------------------------------------------------------------------
 // chain_kernel<KMAX, CB>: the pivots of one window (npiv <= KMAX slots),
 // single GPU (row0 = 0).  grid = B blocks of CB threads (one block per CU,
 // every block resident); block b owns columns [b*cpb, ...) and rows
@@ -535,8 +369,8 @@ __device__ __forceinline__ void spec_wait(SpecBox* sb, int pid, State* st, Addr 
 // previous window's chain); the chain writes one partial per block there for
 // the next window.
 // ---------------------------------------------------------------------------
-template <int KMAX, int CB, bool SPEC = false>
-__global__ __launch_bounds__(SPEC ? CB + 64 : CB) void chain_kernel(
+template <int KMAX, int CB>
+__global__ __launch_bounds__(CB) void chain_kernel(
     Key* __restrict__ enter_part, State* st, const Params* __restrict__ prm, int n_ep,
     const double* __restrict__ A, int64_t ld, int64_t m, int64_t N, double* __restrict__ obj,
     Window win, int npiv, int64_t* __restrict__ basis, int64_t* __restrict__ hist,
@@ -551,7 +385,6 @@ __global__ __launch_bounds__(SPEC ? CB + 64 : CB) void chain_kernel(
   __shared__ int bc_blk;
   __shared__ KeyP sk[NW];       // the waves' best keys (payload b = wave index)
   __shared__ double hl[NW][34];  // their winners' histories (+ [33]: the row's RHS)
-  __shared__ SpecBox sbox;       // SPEC: the comm wave's posts
   gu64* gr_enter = (gu64*)gr_enter_;
   gu64* gr_ratio = (gu64*)gr_ratio_;
   const int B = gridDim.x;
@@ -559,10 +392,7 @@ __global__ __launch_bounds__(SPEC ? CB + 64 : CB) void chain_kernel(
   const int t = threadIdx.x;
   const int lane = t & 63;
   const int w = t >> 6;
-  // the wave that publishes and polls: wave 0, or (SPEC) a dedicated comm wave
-  // (threads CB .. CB+63: no row, no column) while waves 0..NW-1 compute
-  const bool w0 = SPEC ? t >= CB : t < 64;
-  const bool comp = !SPEC || t < CB;  // owns a column / row slot
+  const bool w0 = t < 64;
   const bool leader = b == 0 && t == 0;
   // --- everything that does not depend on a pivot, in one batch ---
   const int32_t status0 = st->status;
@@ -595,10 +425,6 @@ __global__ __launch_bounds__(SPEC ? CB + 64 : CB) void chain_kernel(
   for (int s = 0; s < KMAX; ++s) fs[s] = ps[s] = 0.0;
   int64_t slot_r = 0, slot_c = -1;      // lane s: (r_s, c_s)
   if (t == 0) lds_pin[b & 127] = 0.0;
-  if constexpr (SPEC) {
-    if (t == 0) sbox.ctl = -1;
-    __syncthreads();  // the control word before any wave reads it
-  }
   if (status0 != ST_RUNNING) {          // grid-uniform: no pivot in this window
     if (leader)
       for (int s = 0; s < npiv; ++s) win.made[s] = 0;  // (the flush counts made slots)
@@ -621,8 +447,6 @@ __global__ __launch_bounds__(SPEC ? CB + 64 : CB) void chain_kernel(
     int64_t c;
     double zc;
     int wb = 0;
-    double fv_spec = 0.0;  // SPEC: column c's stale value, loaded at its first post
-    ExRaw<0> ex_spec0;
     if (q == 0) {
       // entering partials of the previous kernel (visible: kernel boundary)
       Keys8 kk;
@@ -631,22 +455,6 @@ __global__ __launch_bounds__(SPEC ? CB + 64 : CB) void chain_kernel(
       wave_min_dpp(e);
       c = e.row;
       zc = c >= 0 ? obj[c] : 0.0;
-    } else if constexpr (SPEC) {
-      if (w0) {
-        KeyP e;
-        const bool ok = poll_spec<false, 3>(gr_enter, B, rec_tag(W, q - 1, GK_ENTER), rule, e,
-                                            st, &sbox, 2 * q);
-        c = ok ? e.row : -2;
-        zc = e.a;
-        wb = (int)e.b;
-        SPX_PROBE_CHAIN(q - 1, 3);
-      } else {
-        int64_t ci;
-        spec_wait<0>(&sbox, 2 * q, st, [&](int64_t x) { return A + x * ld + ic; }, gr_enter,
-                     ENTER_HDR, q, 0, ci, wb, zc, fv_spec, ex_spec0);
-        c = ci;
-      }
-      if (c == -2) return;  // a wait timed out (ST_FAULT stored)
     } else {
       if (w0) {
         KeyP e;
@@ -676,22 +484,12 @@ __global__ __launch_bounds__(SPEC ? CB + 64 : CB) void chain_kernel(
     if (stop_status != ST_RUNNING) break;  // grid-uniform
     // column c on my row: stale + pending slots, in slot order; p_s[c] (lane
     // s) from the winning entering record's history
-    double fv = 0.0, pcl = 0.0, unused[2];
-    if (comp) {
-      if (SPEC && q > 0) {
-        fv = fv_spec;
-        if (!extras_ok<0>(ex_spec0, q, rec_tag(W, q - 1, GK_ENTER), pcl, unused) &&
-            !load_extras<0>(gr_enter, wb, ENTER_HDR, q, 0, rec_tag(W, q - 1, GK_ENTER), pcl,
-                            unused, st))
-          return;
-      } else {
-        fv = A[c * ld + ic];
-        if (q > 0 &&
-            !load_extras<0>(gr_enter, wb, ENTER_HDR, q, 0, rec_tag(W, q - 1, GK_ENTER), pcl,
-                            unused, st))
-          return;
-      }
-    }
+    double fv = A[c * ld + ic];
+    double pcl = 0.0, unused[2];
+    if (q > 0 &&
+        !load_extras<0>(gr_enter, wb, ENTER_HDR, q, 0, rec_tag(W, q - 1, GK_ENTER), pcl, unused,
+                        st))
+      return;
     SPX_PROBE(q, 2, 0, fv != 12345.678 && pcl != 12345.678);  // loads arrived
     // RHS: apply slot q-1 (the slots before it are already in bcur)
     if (q > 0) bcur = apply_sel(bcur, i == r_prev, false, true, f_prev, prhs, skip);
@@ -731,7 +529,7 @@ __global__ __launch_bounds__(SPEC ? CB + 64 : CB) void chain_kernel(
         if (s <= q) hl[w][s] = fs[s];
       hl[w][33] = bcur;
     }
-    if (comp && lane == 0) sk[w] = KeyP{k.v, k.t, k.row, 0.0, (double)w};
+    if (lane == 0) sk[w] = KeyP{k.v, k.t, k.row, 0.0, (double)w};
     __syncthreads();
     if (w0) {
       publish_record<NW, true>(gr_ratio, b, rec_tag(W, q, GK_RATIO), q + 1, sk, hl);
@@ -743,41 +541,21 @@ __global__ __launch_bounds__(SPEC ? CB + 64 : CB) void chain_kernel(
     SPX_PROBE(q, 0, 3, true);
     // ================= norm phase q =================
     SPX_PROBE(q, 1, 0, true);
-    int64_t r;
-    double v_spec = 0.0;  // SPEC: row r's stale value, loaded at its first post
-    ExRaw<1> ex_spec1;
-    if constexpr (SPEC) {
+    if (w0) {
+      KeyP rk;
       const unsigned rtag = rec_tag(W, q, GK_RATIO);
-      if (w0) {
-        KeyP rk;
-        const bool ok = rule == RULE_BLAND
-                            ? poll_spec<true, 4>(gr_ratio, B, rtag, rule, rk, st, &sbox, 2 * q + 1)
-                            : poll_spec<true, 3>(gr_ratio, B, rtag, rule, rk, st, &sbox, 2 * q + 1);
-        r = ok ? rk.row : -2;
-        wb = (int)rk.b;
-        SPX_PROBE_CHAIN(q, 1);
-      } else {
-        double unused_v;
-        spec_wait<1>(&sbox, 2 * q + 1, st, [&](int64_t x) { return A + jc * ld + x; }, gr_ratio,
-                     RATIO_HDR + 2, q + 1, RATIO_HDR, r, wb, unused_v, v_spec, ex_spec1);
+      const bool ok = rule == RULE_BLAND
+                          ? poll_records<true, 4>(gr_ratio, B, rtag, rule, rk, st)
+                          : poll_records<true, 3>(gr_ratio, B, rtag, rule, rk, st);
+      if (t == 0) {
+        bc_idx = ok ? rk.row : -2;
+        bc_blk = (int)rk.b;
       }
-    } else {
-      if (w0) {
-        KeyP rk;
-        const unsigned rtag = rec_tag(W, q, GK_RATIO);
-        const bool ok = rule == RULE_BLAND
-                            ? poll_records<true, 4>(gr_ratio, B, rtag, rule, rk, st)
-                            : poll_records<true, 3>(gr_ratio, B, rtag, rule, rk, st);
-        if (t == 0) {
-          bc_idx = ok ? rk.row : -2;
-          bc_blk = (int)rk.b;
-        }
-        SPX_PROBE_CHAIN(q, 1);
-      }
-      __syncthreads();
-      r = bc_idx;
-      wb = bc_blk;
+      SPX_PROBE_CHAIN(q, 1);
     }
+    __syncthreads();
+    const int64_t r = bc_idx;
+    wb = bc_blk;
     if (r == -2) return;
     SPX_PROBE(q, 1, 1, true);
     if (q == 0 && leader) *win.epoch = W;  // every block has read E (its record carries W)
@@ -787,21 +565,11 @@ __global__ __launch_bounds__(SPEC ? CB + 64 : CB) void chain_kernel(
     }
     // row r on my column: stale + pending slots.  f_s[r] (lane s <= q, lane q
     // the pivot element) and the row's RHS from the winning ratio record
-    double v = 0.0, frl = 0.0, ex[2] = {0.0, 0.0};
-    if (comp) {
-      if (SPEC) {
-        v = v_spec;
-        if (!extras_ok<1>(ex_spec1, q + 1, rec_tag(W, q, GK_RATIO), frl, ex) &&
-            !load_extras<1>(gr_ratio, wb, RATIO_HDR + 2, q + 1, RATIO_HDR,
-                            rec_tag(W, q, GK_RATIO), frl, ex, st))
-          return;
-      } else {
-        v = A[jc * ld + r];
-        if (!load_extras<1>(gr_ratio, wb, RATIO_HDR + 2, q + 1, RATIO_HDR,
-                            rec_tag(W, q, GK_RATIO), frl, ex, st))
-          return;
-      }
-    }
+    double v = A[jc * ld + r];
+    double frl = 0.0, ex[2];
+    if (!load_extras<1>(gr_ratio, wb, RATIO_HDR + 2, q + 1, RATIO_HDR, rec_tag(W, q, GK_RATIO),
+                        frl, ex, st))
+      return;
     SPX_PROBE(q, 3, 0, v != 12345.678 && frl != 12345.678);  // loads arrived
     const double piv = rdlane(frl, q);
     prhs = ex[0] / piv;  // p_q[rhs]: lazy_norm's p = v / piv of the RHS column
@@ -857,12 +625,12 @@ __global__ __launch_bounds__(SPEC ? CB + 64 : CB) void chain_kernel(
       for (int s = 0; s < KMAX; ++s)
         if (s <= q) hl[w][s] = ps[s];
     }
-    if (comp && lane == 0) sk[w] = KeyP{ek.v, ek.t, ek.row, ek.a, (double)w};
+    if (lane == 0) sk[w] = KeyP{ek.v, ek.t, ek.row, ek.a, (double)w};
     __syncthreads();
     if (w0) {
       if (q + 1 < npiv) {
         publish_record<NW, false>(gr_enter, b, rec_tag(W, q, GK_ENTER), q + 1, sk, hl);
-      } else if (lane == 0) {
+      } else if (t == 0) {
         // the next window's pivot-0 partial (read after the kernel boundary)
         KeyP kb = sk[0];
 #pragma unroll
@@ -908,7 +676,7 @@ __global__ __launch_bounds__(SPEC ? CB + 64 : CB) void chain_kernel(
   __shared__ int wcnt[NW];
   __shared__ int base;
   const uint64_t bal = __ballot(mine);
-  if (comp && lane == 0) wcnt[w] = __popcll(bal);
+  if (lane == 0) wcnt[w] = __popcll(bal);
   __syncthreads();
   if (t == 0) {
     int tot = 0;
@@ -919,7 +687,7 @@ __global__ __launch_bounds__(SPEC ? CB + 64 : CB) void chain_kernel(
   }
   __syncthreads();
   int pos = base + __popcll(bal & ((1ull << lane) - 1ull));
-  for (int x = 0; x < w && x < NW; ++x) pos += wcnt[x];
+  for (int x = 0; x < w; ++x) pos += wcnt[x];
   if (mine && pos < N) {
     double* rc_ = win.rec + (int64_t)pos * RECW;
     reinterpret_cast<int64_t*>(rc_)[0] = j | ((int64_t)(tg >> 30) << 32);

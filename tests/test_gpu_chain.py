@@ -2,9 +2,7 @@
 runs a window's K pivot choices, with in-launch record exchanges instead of two
 launches per pivot.  It must be BYTE-identical to the launch-per-phase chain
 (mode 1) and to the single-pivot engine: pivot sequence, basis, status and the
-tableau (tobytes), and np.array_equal to the CPU oracle.  Mode 4 adds a
-communication wave that posts speculative exchange winners; the compute waves
-load for every post and keep only the final winner's data.
+tableau (tobytes), and np.array_equal to the CPU oracle.
 """
 import threading
 
@@ -49,7 +47,7 @@ def _run(eng_cls, T, basis, K, mode, min_blocks=0, **kw):
 @pytest.mark.parametrize("K", [2, 8, 16, 24, 32])
 @pytest.mark.parametrize("shape", [(2, 3), (17, 40), (300, 700), (1025, 2051)])
 @pytest.mark.parametrize("rule", ["dantzig", "bland"])
-@pytest.mark.parametrize("mode", [2, 3, 4], ids=["cb256", "cb512", "spec"])
+@pytest.mark.parametrize("mode", [2, 3], ids=["cb256", "cb512"])
 def test_chain_matches_lazy_chain_and_oracle(eng_cls, K, shape, rule, mode):
     T, basis = _random_tableau(*shape, seed=shape[0] * 7 + K)
     kw = dict(max_iters=3 * K + 5, rule=rule)
@@ -65,18 +63,17 @@ def test_chain_matches_lazy_chain_and_oracle(eng_cls, K, shape, rule, mode):
 
 
 @pytest.mark.parametrize("min_blocks", [0, 3, 64, 100, 256])
-@pytest.mark.parametrize("mode", [0, 4])
-def test_chain_grid_sizes_bit_exact(eng_cls, min_blocks, mode):
+def test_chain_grid_sizes_bit_exact(eng_cls, min_blocks):
     """More blocks than the minimum (fewer columns / rows per block, more than
     64 records per poll) give the same bytes."""
     T, basis = _random_tableau(400, 1300, seed=11 + min_blocks)
-    res, h, out, b, blocks = _run(eng_cls, T, basis, 16, mode, min_blocks, max_iters=53)
+    res, h, out, b, blocks = _run(eng_cls, T, basis, 16, 0, min_blocks, max_iters=53)
     res1, h1, out1, b1, _ = _run(eng_cls, T, basis, 16, 1, max_iters=53)
-    assert blocks == max(min_blocks, 7 if mode == 4 else 6)
+    assert blocks == max(min_blocks, 6)
     assert h == h1 and res.iters == res1.iters and out.tobytes() == out1.tobytes()
 
 
-@pytest.mark.parametrize("mode,nb", [(0, 80), (2, 80), (3, 40), (4, 107)])
+@pytest.mark.parametrize("mode,nb", [(0, 80), (2, 80), (3, 40)])
 def test_chain_wide_tableau_more_than_64_blocks(eng_cls, mode, nb):
     """N > 64 x 256 columns: B = 80 blocks of 256 threads (two records per
     polling lane; the automatic choice), or 40 of 512."""
@@ -88,11 +85,10 @@ def test_chain_wide_tableau_more_than_64_blocks(eng_cls, mode, nb):
 
 
 @pytest.mark.parametrize("K", [4, 32])
-@pytest.mark.parametrize("mode", [0, 4])
-def test_chain_degenerate_bland_full_solve(eng_cls, K, mode):
+def test_chain_degenerate_bland_full_solve(eng_cls, K):
     from simplex_amd import synth
     T, basis = synth.full_tableau("degenerate", 96, 96, seed=3)
-    res, h, out, b, _ = _run(eng_cls, T, basis, K, mode, rule="bland")
+    res, h, out, b, _ = _run(eng_cls, T, basis, K, 0, rule="bland")
     res1, h1, out1, b1, _ = _run(eng_cls, T, basis, K, 1, rule="bland")
     ref, rb = T.copy(), basis.copy()
     st, hist = O.solve_tableau(ref, rb, rule="bland")
@@ -101,13 +97,12 @@ def test_chain_degenerate_bland_full_solve(eng_cls, K, mode):
     assert out.tobytes() == out1.tobytes() and np.array_equal(out, ref)
 
 
-@pytest.mark.parametrize("mode", [0, 4])
-def test_chain_stops_inside_window(eng_cls, mode):
+def test_chain_stops_inside_window(eng_cls):
     """Optimal, unbounded and the iteration limit inside a window."""
     # optimal after a few pivots
     T, basis = _random_tableau(30, 80, seed=9)
     for mi in (0, 5, 13):
-        r0 = _run(eng_cls, T, basis, 32, mode, max_iters=mi)
+        r0 = _run(eng_cls, T, basis, 32, 0, max_iters=mi)
         r1 = _run(eng_cls, T, basis, 32, 1, max_iters=mi)
         assert r0[0].status == r1[0].status and r0[1] == r1[1]
         assert r0[2].tobytes() == r1[2].tobytes()
@@ -116,7 +111,7 @@ def test_chain_stops_inside_window(eng_cls, mode):
     n = 50 - 1 - 19
     T2[:19, 3] = -np.abs(T2[:19, 3]) - 0.1
     T2[19, 3] = -50.0
-    r0 = _run(eng_cls, T2, b2, 8, mode)
+    r0 = _run(eng_cls, T2, b2, 8, 0)
     r1 = _run(eng_cls, T2, b2, 8, 1)
     ref, rb = T2.copy(), b2.copy()
     st, hist = O.solve_tableau(ref, rb)
@@ -130,7 +125,7 @@ def test_chain_resume_across_calls(eng_cls):
     """Several calls on one context (iteration limits mid-window, pivot_at)."""
     T, basis = _random_tableau(200, 600, seed=21)
     outs = []
-    for mode in (0, 1, 4):
+    for mode in (0, 1):
         with eng_cls(0) as e:
             e.set_window(16)
             e.set_chain(mode)
@@ -140,17 +135,16 @@ def test_chain_resume_across_calls(eng_cls):
             e.pivot()
             e.solve(max_iters=30)
             outs.append((e.history().tolist(), e.tableau().tobytes(), e.basis().tolist()))
-    assert outs[0] == outs[1] == outs[2]
+    assert outs[0] == outs[1]
 
 
-@pytest.mark.parametrize("mode", [0, 4])
-def test_chain_concurrent_contexts(eng_cls, mode):
+def test_chain_concurrent_contexts(eng_cls):
     """Two contexts' persistent chains on two streams at once."""
     T, basis = _random_tableau(500, 1500, seed=33)
     res = [None, None]
 
     def work(k):
-        res[k] = _run(eng_cls, T, basis, 24, mode, max_iters=100)
+        res[k] = _run(eng_cls, T, basis, 24, 0, max_iters=100)
 
     th = [threading.Thread(target=work, args=(k,)) for k in range(2)]
     for x in th:
@@ -165,6 +159,6 @@ def test_chain_concurrent_contexts(eng_cls, mode):
 def test_chain_set_validated(eng_cls):
     with eng_cls(0) as e:
         with pytest.raises(Exception):
-            e.set_chain(5)
+            e.set_chain(4)
         with pytest.raises(Exception):
             e.set_chain(0, 300)
