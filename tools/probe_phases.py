@@ -62,7 +62,7 @@ def main():
     t = lambda slot, kind, ph: buf[((slot * 4 + kind) * 4 + ph) & 1023]
     t0 = t(0, 0, 0)
     us = lambda x: (x - t0) / 100.0
-    names = ({0: "lazy_ratio", 1: "lazy_norm"} if a.chain else
+    names = ({0: "lazy_ratio", 1: "lazy_norm"} if a.chain == 1 else
              {0: "ratio ph.", 1: "norm ph."})
     print(f"window K={K}, m={a.m}, n={a.n}: us from lazy_ratio(0) entry (block 0, thread 0)")
     prev_end = None
@@ -74,14 +74,14 @@ def main():
                   f"  phase1 +{ph[1]-ph[0]:5.2f}  phase2 +{ph[2]-ph[1]:5.2f}"
                   f"  end +{ph[3]-ph[2]:5.2f}  total {ph[3]-ph[0]:5.2f}")
             prev_end = ph[3]
-            if not a.chain and t(q, 2 + kind, 0) > t0:
+            if a.chain != 1 and t(q, 2 + kind, 0) > t0:
                 a0, a1 = us(t(q, 2 + kind, 0)), us(t(q, 2 + kind, 1))
                 print(f"       fine: loads arrived +{a0 - ph[1]:5.2f}  slots applied "
                       f"+{a1 - a0:5.2f}  rest of phase2 +{ph[2] - a1:5.2f}")
             if kind == 0 and os.environ.get("SPX_PROBE_FINE"):
                 k0, k1 = us(t(q, 2, 0)), us(t(q, 2, 1))
                 print(f"       fine: keys reduced +{k0 - ph[0]:5.2f}  wave_min +{k1 - k0:5.2f}")
-    if not a.chain:
+    if a.chain != 1:
         nb = e.chain_blocks()
         cb = (ctypes.c_ulonglong * (32 * 4 * 256))()
         assert lib.spx_probe_read_chain(cb, 32 * 4 * 256) == 0
