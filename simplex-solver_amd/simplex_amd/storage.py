@@ -1,37 +1,244 @@
-"""Minimal report sink with the reference's ``StorageService.save_solution`` seam.
+"""Report persistence with the reference's ``StorageService`` API.
 
-The reference persists the report as sequential ``outputs/solucion_N.json``
-files (app/services/storage_service.py:34-42, :75-88, :106-112).  Storage is out
-of scope for this build; this keeps only the static ``save_solution`` entry the
-controller calls once per solve (solver_controller.py:426) and that the
-reference tests patch (tests/test_solver_controller.py:126).  File names are
-claimed with O_EXCL, so concurrent solves cannot overwrite each other (the
-reference's _get_next_filename has a check-then-write race).
+Mirrors ``app/services/storage_service.py`` (reference): sequential files
+``outputs/<prefix><N>.json`` under the same prefixes (``app/config.py:20-24``),
+the same save / load-latest entry points and the same return values
+(``save_*`` -> path, ``load_*`` -> data, ``FileNotFoundError`` when nothing was
+saved yet, ``None`` for an unreadable file).  The controller calls
+``save_solution`` once per solve (``solver_controller.py:426``); the reference
+tests patch that static method (``tests/test_solver_controller.py:126``).
+
+What changes, for many concurrent ``/solve`` calls and large reports:
+
+* **No check-then-write race.**  The reference picks the first number whose
+  file does not exist (``storage_service.py:34-42``) and opens it later, so two
+  concurrent solves can pick the same name and one report overwrites the other.
+  Here a number is claimed by creating the file with ``O_CREAT | O_EXCL``; the
+  content goes to a private temporary file that replaces the claimed name
+  atomically, so a reader never sees a half-written report.
+* **Latest = latest complete.**  ``load_*`` take the highest-numbered file that
+  holds a complete document; a number that is claimed but still being written
+  (an empty placeholder) is skipped instead of raising ``JSONDecodeError``.
+* **Bounded writes.**  ``json.dump`` streams to the file (the report is never
+  rendered as one string).  Long numeric tables (``tablas_intermedias`` rows,
+  pivot histories) are written one row per line instead of one number per line
+  as ``indent=4`` would (the byte count of a 2M-cell history drops ~3x), and the
+  engine already caps snapshots at 2,000,000 cells.
+
+Storage is a sink of the hot path, not part of it: nothing here touches the GPU.
 """
 from __future__ import annotations
 
 import json
 import os
+import re
+import tempfile
+from typing import Any, Dict, List, Optional
 
 OUTPUT_DIR = os.environ.get("SPX_OUTPUT_DIR", os.path.join(os.getcwd(), "outputs"))
-PREFIX_SOLUTION = "solucion_"
+# the reference's prefixes (app/config.py:20-24)
+PREFIX_FUNCION_OBJETIVO = "funcion_objetivo"
+PREFIX_RESTRICCIONES = "restricciones"
+PREFIX_SOLUCION = "solucion_"
+PREFIX_PROBLEMA = "problema_"
+PREFIX_PDF = "reporte_solucion_"
+# kept for callers of the round-1 module
+PREFIX_SOLUTION = PREFIX_SOLUCION
+
+
+def _out_dir() -> str:
+    return OUTPUT_DIR
 
 
 class StorageService:
+    """Sequential JSON files in OUTPUT_DIR (reference: storage_service.py:24-182)."""
+
+    def __init__(self):
+        # (the reference creates OUTPUT_DIR here; this build creates it on the
+        # first save, so constructing a controller has no file-system effect)
+        pass
+
+    # --- file names -------------------------------------------------------
+
     @staticmethod
-    def save_solution(report: dict) -> str:
-        os.makedirs(OUTPUT_DIR, exist_ok=True)
-        k = 1
+    def _claim_next_filename(prefix: str, extension: str = ".json") -> str:
+        """Create and return the first free ``<prefix><N><extension>`` (O_EXCL:
+        the name belongs to this caller even under concurrent claims)."""
+        d = _out_dir()
+        os.makedirs(d, exist_ok=True)
+        number = 1
         while True:
-            path = os.path.join(OUTPUT_DIR, f"{PREFIX_SOLUTION}{k}.json")
+            path = os.path.join(d, f"{prefix}{number}{extension}")
             try:
                 fd = os.open(path, os.O_WRONLY | os.O_CREAT | os.O_EXCL, 0o644)
             except FileExistsError:
-                k += 1
+                number += 1
                 continue
-            with os.fdopen(fd, "w", encoding="utf-8") as f:
-                json.dump(report, f, ensure_ascii=False, indent=2, default=_jsonable)
+            os.close(fd)
             return path
+
+    @staticmethod
+    def _get_next_filename(prefix: str, extension: str = ".json") -> str:
+        """The reference's name picker (storage_service.py:34-42), race-free: the
+        returned name is claimed (an empty file exists under it)."""
+        return StorageService._claim_next_filename(prefix, extension)
+
+    @staticmethod
+    def _numbered(prefix: str, extension: str) -> List[tuple]:
+        d = _out_dir()
+        if not os.path.exists(d):
+            return []
+        pat = re.compile(f"^{re.escape(prefix)}(\\d+){re.escape(extension)}$")
+        out = []
+        for f in os.listdir(d):
+            m = pat.match(f)
+            if m:
+                out.append((int(m.group(1)), os.path.join(d, f)))
+        out.sort()
+        return out
+
+    @staticmethod
+    def _get_latest_filename(prefix: str, extension: str = ".json") -> Optional[str]:
+        """Highest-numbered ``<prefix><N><extension>`` that is not an empty
+        placeholder (storage_service.py:44-72), or None."""
+        for _, path in reversed(StorageService._numbered(prefix, extension)):
+            try:
+                if os.path.getsize(path) > 0:
+                    return path
+            except OSError:
+                continue
+        return None
+
+    # --- save -------------------------------------------------------------
+
+    @staticmethod
+    def save_json(data: Any, prefix: str, extension: str = ".json") -> Optional[str]:
+        """Write ``data`` to a new sequential file; the path, or None on an I/O
+        error (the reference prints the error and returns None, :76-88)."""
+        filename = StorageService._claim_next_filename(prefix, extension)
+        try:
+            _write_atomic(filename, data)
+            return filename
+        except (IOError, OSError) as e:
+            print(f"Error al guardar el archivo {filename}: {e}")
+            return None
+
+    @staticmethod
+    def save_constraints(constraints: List[Dict]) -> Optional[str]:
+        return StorageService.save_json(constraints, prefix=PREFIX_RESTRICCIONES)
+
+    @staticmethod
+    def save_objective_function(objective_data: Dict) -> Optional[str]:
+        return StorageService.save_json(objective_data, prefix=PREFIX_FUNCION_OBJETIVO)
+
+    @staticmethod
+    def save_solution(report_data: Dict) -> Optional[str]:
+        return StorageService.save_json(report_data, prefix=PREFIX_SOLUCION)
+
+    @staticmethod
+    def save_problem(problem_data: dict) -> Optional[str]:
+        return StorageService.save_json(problem_data, prefix=PREFIX_PROBLEMA)
+
+    # --- load -------------------------------------------------------------
+
+    @staticmethod
+    def load_json(prefix: str) -> Any:
+        """Data of the latest complete ``<prefix><N>.json`` (storage_service.py:
+        124-144): FileNotFoundError if none, None if it cannot be parsed."""
+        filename = StorageService._get_latest_filename(prefix, extension=".json")
+        if not filename or not os.path.exists(filename):
+            raise FileNotFoundError(
+                f"No se encontró ningún archivo con prefijo '{prefix}' en {_out_dir()}.")
+        try:
+            with open(filename, "r", encoding="utf-8") as f:
+                return json.load(f)
+        except json.JSONDecodeError:
+            print(f"Error: El archivo {filename} está corrupto o mal formateado.")
+            return None
+        except IOError as e:
+            print(f"Error al leer el archivo {filename}: {e}")
+            return None
+
+    @staticmethod
+    def load_constraints() -> List[Dict]:
+        return StorageService.load_json(prefix=PREFIX_RESTRICCIONES)
+
+    @staticmethod
+    def load_objective_function() -> Dict:
+        return StorageService.load_json(prefix=PREFIX_FUNCION_OBJETIVO)
+
+    @staticmethod
+    def load_problem() -> dict:
+        return StorageService.load_json(prefix=PREFIX_PROBLEMA)
+
+    @staticmethod
+    def load_solution() -> dict:
+        return StorageService.load_json(prefix=PREFIX_SOLUCION)
+
+    @staticmethod
+    def get_new_pdf_path() -> str:
+        """A claimed path for the next PDF report (storage_service.py:176-179)."""
+        return StorageService._claim_next_filename(prefix=PREFIX_PDF, extension=".pdf")
+
+
+# --- writing --------------------------------------------------------------
+
+def _write_atomic(path: str, data: Any) -> None:
+    """Stream ``data`` as JSON to a temporary file beside ``path``, then move it
+    over ``path`` (a reader sees the empty claim or the whole document)."""
+    d = os.path.dirname(path) or "."
+    fd, tmp = tempfile.mkstemp(prefix=".tmp_", suffix=".json", dir=d)
+    try:
+        with os.fdopen(fd, "w", encoding="utf-8") as f:
+            _dump(data, f, 0)
+            f.write("\n")
+        os.replace(tmp, path)
+    except BaseException:
+        try:
+            os.unlink(tmp)
+        except OSError:
+            pass
+        raise
+
+
+_IND = "    "  # the reference's indent=4
+
+
+def _scalar(x) -> bool:
+    return x is None or isinstance(x, (bool, int, float, str))
+
+
+def _dump(o: Any, f, level: int) -> None:
+    """``json.dump(o, indent=4, ensure_ascii=False)`` except that a list of
+    scalars (a table row, a pivot pair) goes on one line, streamed piecewise."""
+    o = _jsonable(o) if not isinstance(o, (dict, list, str, int, float, bool, type(None))) else o
+    if isinstance(o, dict):
+        if not o:
+            f.write("{}")
+            return
+        f.write("{\n")
+        n = len(o)
+        for k, (key, val) in enumerate(o.items()):
+            f.write(_IND * (level + 1) + json.dumps(str(key), ensure_ascii=False) + ": ")
+            _dump(val, f, level + 1)
+            f.write(",\n" if k + 1 < n else "\n")
+        f.write(_IND * level + "}")
+    elif isinstance(o, list):
+        if not o:
+            f.write("[]")
+            return
+        if all(_scalar(x) for x in o):
+            f.write(json.dumps(o, ensure_ascii=False, allow_nan=True))
+            return
+        f.write("[\n")
+        n = len(o)
+        for k, val in enumerate(o):
+            f.write(_IND * (level + 1))
+            _dump(val, f, level + 1)
+            f.write(",\n" if k + 1 < n else "\n")
+        f.write(_IND * level + "]")
+    else:
+        f.write(json.dumps(o, ensure_ascii=False, allow_nan=True))
 
 
 def _jsonable(o):

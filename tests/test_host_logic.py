@@ -2,6 +2,7 @@
 simple_simplex text API, the SolverController contract (reference
 tests/test_solver_controller.py re-expressed with unittest.mock)."""
 import io
+import os
 from contextlib import redirect_stdout
 from unittest import mock
 
@@ -194,3 +195,80 @@ def test_auto_window_by_size():
     assert auto_window(8192, 16385) == 24        # config 3
     for m, n in ((0, 0), (10, 10), (2000, 600), (5000, 20000), (100000, 200000)):
         assert auto_window(m, n) in (0, 8, 16, 24)
+
+
+# --- report persistence (simplex_amd/storage.py) ---------------
+
+def test_storage_roundtrip_and_latest(tmp_path, monkeypatch):
+    """save_* / load_* mirror app/services/storage_service.py: sequential names
+    per prefix, load_* returns the highest-numbered complete document."""
+    import json
+    from simplex_amd import storage
+    S = storage.StorageService
+    monkeypatch.setattr(storage, "OUTPUT_DIR", str(tmp_path))
+    with pytest.raises(FileNotFoundError):
+        S.load_solution()
+    rep = {"problema_definicion": {"funcion_objetivo": {"type": "maximize"}},
+           "tablas_intermedias": [{"iteration": 0, "table": [["F0", 1.0, np.float64(2.5)],
+                                                           ["F1", -0.0, float("nan")]],
+                                   "pivot": (1, 2)}],
+           "valor": np.float32(3.0), "arr": np.arange(3)}
+    p1 = S.save_solution(rep)
+    p2 = S.save_solution({"n": 2})
+    assert p1.endswith("solucion_1.json") and p2.endswith("solucion_2.json")
+    assert S.load_solution() == {"n": 2}
+    back = json.load(open(p1, encoding="utf-8"))
+    t = back["tablas_intermedias"][0]
+    assert t["pivot"] == [1, 2] and t["table"][0] == ["F0", 1.0, 2.5]
+    assert back["valor"] == 3.0 and back["arr"] == [0, 1, 2]
+    assert np.isnan(t["table"][1][2]) and str(t["table"][1][1]) == "-0.0"
+    # a table row is one line (indent=4 would put every number on its own line)
+    assert '["F0", 1.0, 2.5]' in open(p1, encoding="utf-8").read()
+    for save, load in ((S.save_problem, S.load_problem), (S.save_constraints, S.load_constraints),
+                       (S.save_objective_function, S.load_objective_function)):
+        save({"k": [1, 2]})
+        assert load() == {"k": [1, 2]}
+    assert S.get_new_pdf_path().endswith("reporte_solucion_1.pdf")
+    assert S.get_new_pdf_path().endswith("reporte_solucion_2.pdf")
+
+
+def test_storage_latest_skips_claimed_placeholder(tmp_path, monkeypatch):
+    """A number claimed by a solve still writing (empty file) is not 'latest'."""
+    from simplex_amd import storage
+    S = storage.StorageService
+    monkeypatch.setattr(storage, "OUTPUT_DIR", str(tmp_path))
+    S.save_solution({"v": 1})
+    claimed = S._get_next_filename(storage.PREFIX_SOLUCION)
+    assert claimed.endswith("solucion_2.json") and (tmp_path / "solucion_2.json").exists()
+    assert S.load_solution() == {"v": 1}
+    assert S.save_solution({"v": 3}).endswith("solucion_3.json")
+    assert S.load_solution() == {"v": 3}
+    (tmp_path / "solucion_4.json").write_text("{ not json")
+    assert S.load_solution() is None   # the reference prints and returns None
+
+
+def test_storage_concurrent_saves_unique_and_complete(tmp_path, monkeypatch):
+    """Many threads saving at once (the reference's _get_next_filename can hand
+    two of them one name): every report lands in its own complete file."""
+    import json
+    import threading
+    from simplex_amd import storage
+    S = storage.StorageService
+    monkeypatch.setattr(storage, "OUTPUT_DIR", str(tmp_path))
+    paths, errs = [], []
+
+    def work(k):
+        try:
+            paths.append(S.save_solution({"k": k, "rows": [[k] * 50] * 20}))
+        except Exception as e:  # pragma: no cover
+            errs.append(e)
+
+    th = [threading.Thread(target=work, args=(k,)) for k in range(32)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    assert not errs and len(set(paths)) == 32
+    ks = sorted(json.load(open(p, encoding="utf-8"))["k"] for p in paths)
+    assert ks == list(range(32))
+    assert not [f for f in os.listdir(tmp_path) if f.startswith(".tmp_")]
