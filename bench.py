@@ -218,6 +218,26 @@ def main():
     if status != 4 or iters != n_warm + n_timed:
         raise SystemExit(f"pivot loop ended early: status {status}, iters {iters}")
     ms_tot, launches, touched = eng.elim_timing(reset=True)
+    chain = None
+    if K and world == 1:
+        # the pivot chain, the other half of a window: HIP events around each
+        # window's chain in 8 windows AFTER the timed region (event nodes cost
+        # stream time, so they stay out of `value`)
+        eng.set_chain_timing(True)
+        eng.run_pivots(8 * K, **opts)
+        eng.sync()
+        c_ms, c_n = eng.chain_timing(reset=True)
+        eng.set_chain_timing(False)
+        nb = eng.chain_blocks()
+        chain = {"kernel": "spx::chain_kernel" if nb else
+                 "spx::lazy_ratio_kernel + spx::lazy_norm_kernel",
+                 "bound": "latency: two in-launch all-to-all exchanges and two dependent "
+                          "HBM gathers per pivot (DESIGN.md 4b)",
+                 "blocks": nb, "avg_launch_us": 1e3 * c_ms / max(c_n, 1),
+                 "us_per_pivot": 1e3 * c_ms / max(c_n * K, 1),
+                 "share_of_step": (c_ms / max(c_n, 1)) / (1e3 * elapsed / args.steps),
+                 "window": f"HIP events around the chain of {c_n} windows run after the "
+                           f"timed region"}
     what = "flush (window pass)" if K else "elimination"
     every = f"every {every}th"
     window = (f"timed region: HIP events on the engine stream around {every} {what}, "
@@ -302,6 +322,7 @@ def main():
                          "touched_cols_per_launch": cols_per_launch,
                          "dense_equiv_GBps": dense_bytes / (avg_ms * 1e-3) / 1e9,
                          "window": window},
+            "chain": chain,
             "cpu_baseline": cpu,
             "objective_after": z,
         }

@@ -186,6 +186,12 @@ int spx_get_flush_variant(const spx_ctx* ctx, int64_t out[4]);
  * Results are bit-identical.  Row-sharded contexts run the
  * same windows with one all-gather per pivot. */
 int spx_set_window(spx_ctx* ctx, int K);
+/* Pivot-choice timing (diagnostic): when on, every window records HIP events
+ * around its chain (the persistent kernel, or the lazy kernels of its slots);
+ * spx_chain_timing returns their sum and count since the last reset.  The
+ * event nodes add stream time, so measure it outside a timed region. */
+int spx_set_chain_timing(spx_ctx* ctx, int on);
+int spx_chain_timing(spx_ctx* ctx, double* total_ms, int64_t* count, int reset);
 /* Pivot chain of a window (the K pivot choices before its flush): mode 0
  * (default) runs them as ONE persistent launch when the tableau fits (at most
  * 512 x CUs columns and rows, single-GPU contexts), mode 1 as two

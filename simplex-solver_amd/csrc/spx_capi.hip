@@ -142,6 +142,11 @@ struct spx_ctx {
   // elimination timing
   std::vector<std::pair<hipEvent_t, hipEvent_t>> ev;
   size_t ev_used = 0;
+  // pivot-choice timing (spx_set_chain_timing): events around each window's
+  // chain (the persistent kernel, or the lazy kernels of all its slots)
+  bool time_chain = false;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> evc;
+  size_t evc_used = 0;
   int64_t touched_at_reset = 0;
 };
 
@@ -399,11 +404,30 @@ int chain_blocks(spx_ctx* ctx, int* cb_out = nullptr) {
   return need <= cap ? (int)need : 0;
 }
 
+// An event pair from the context's pool (created on first use).
+int next_event_pair(spx_ctx* ctx, std::vector<std::pair<hipEvent_t, hipEvent_t>>& pool,
+                    size_t& used, std::pair<hipEvent_t, hipEvent_t>** out) {
+  if (used == pool.size()) {
+    hipEvent_t a, b;
+    HIPC(hipEventCreate(&a));
+    HIPC(hipEventCreate(&b));
+    pool.emplace_back(a, b);
+  }
+  *out = &pool[used++];
+  return SPX_OK;
+}
+
 template <int KMAX>
 int enqueue_window_t(spx_ctx* ctx, int npiv, bool time_flush) {
   const int nbw = lazy_ratio_grid(ctx);
   int cb = BLK;
   const int B = chain_blocks(ctx, &cb);
+  std::pair<hipEvent_t, hipEvent_t>* ec = nullptr;
+  if (ctx->time_chain) {
+    int rc = next_event_pair(ctx, ctx->evc, ctx->evc_used, &ec);
+    if (!rc) rc = record_event(ctx, ec->first);
+    if (rc) return rc;
+  }
   if (B > 0) {
     const int cpb = (int)((ctx->N + B - 1) / B);
     const int rpb = (int)((ctx->m_local + B - 1) / B);
@@ -443,16 +467,14 @@ int enqueue_window_t(spx_ctx* ctx, int npiv, bool time_flush) {
                          (const char*)ctx->recvbuf, ctx->gstride, ctx->nranks);
     }
   }
+  if (ec) {
+    const int rc = record_event(ctx, ec->second);
+    if (rc) return rc;
+  }
   std::pair<hipEvent_t, hipEvent_t>* e = nullptr;
   if (time_flush) {
-    if (ctx->ev_used == ctx->ev.size()) {
-      hipEvent_t a, b;
-      HIPC(hipEventCreate(&a));
-      HIPC(hipEventCreate(&b));
-      ctx->ev.emplace_back(a, b);
-    }
-    e = &ctx->ev[ctx->ev_used++];
-    const int rc = record_event(ctx, e->first);
+    int rc = next_event_pair(ctx, ctx->ev, ctx->ev_used, &e);
+    if (!rc) rc = record_event(ctx, e->first);
     if (rc) return rc;
   }
   auto go = [&](auto kern, int rt, int threads = BLK) {
@@ -852,10 +874,11 @@ int spx_destroy(spx_ctx* ctx) {
   (void)hipSetDevice(ctx->device);
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
   free_buffers(ctx);
-  for (auto& e : ctx->ev) {
-    (void)hipEventDestroy(e.first);
-    (void)hipEventDestroy(e.second);
-  }
+  for (auto* pool : {&ctx->ev, &ctx->evc})
+    for (auto& e : *pool) {
+      (void)hipEventDestroy(e.first);
+      (void)hipEventDestroy(e.second);
+    }
   if (ctx->comm) (void)ncclCommDestroy(ctx->comm);
   dfree(ctx->prm);
   dfree(ctx->st);
@@ -1021,7 +1044,7 @@ int spx_solve(spx_ctx* ctx, const spx_opts* opts, spx_result* res) {
   if (rc) return rc;
   const int64_t it0 = ctx->h_st->iters;
   const int chunk = ctx->win_k ? ctx->win_k : (o->chunk > 0 ? o->chunk : 32);
-  const bool use_graph = o->use_graph != 0 && !ctx->loop;
+  const bool use_graph = o->use_graph != 0 && !ctx->loop && !ctx->time_chain;
   if (use_graph) {
     rc = build_graph(ctx, chunk);
     if (rc) return rc;
@@ -1116,7 +1139,9 @@ int spx_run_pivots(spx_ctx* ctx, const spx_opts* opts, int64_t npivots, int time
   const spx_opts* o = opts ? opts : &d;
   int rc = begin_call(ctx, o);
   if (rc) return rc;
-  const bool graph = o->use_graph && !ctx->loop;
+  // (chain timing records one event pair per window: direct launches, since a
+  // replayed graph re-records the same captured events)
+  const bool graph = o->use_graph && !ctx->loop && !ctx->time_chain;
   const int unit = ctx->win_k ? ctx->win_k : 1;  // pivots per enqueue unit
   // the whole request as a sequence of units: full windows, then a remainder
   auto enqueue_all = [&](int tk) -> int {
@@ -1219,6 +1244,31 @@ int spx_state(spx_ctx* ctx, int32_t* status, int64_t* iters, double* objective) 
                         hipMemcpyDeviceToHost, ctx->stream));
     HIPC(hipStreamSynchronize(ctx->stream));
   }
+  return SPX_OK;
+}
+
+// Pivot-choice timing: when on, every window records HIP events around its
+// chain (persistent kernel or lazy kernels).  Diagnostic: the event nodes add
+// stream time, so bench.py measures it in a pass after its timed region.
+int spx_set_chain_timing(spx_ctx* ctx, int on) {
+  if (!ctx) return SPX_E_ARG;
+  ctx->time_chain = on != 0;
+  drop_graphs(ctx);
+  return SPX_OK;
+}
+
+int spx_chain_timing(spx_ctx* ctx, double* total_ms, int64_t* count, int reset) {
+  if (!ctx) return SPX_E_ARG;
+  HIPC(hipStreamSynchronize(ctx->stream));
+  double tot = 0.0;
+  for (size_t i = 0; i < ctx->evc_used; ++i) {
+    float ms = 0.f;
+    HIPC(hipEventElapsedTime(&ms, ctx->evc[i].first, ctx->evc[i].second));
+    tot += ms;
+  }
+  if (total_ms) *total_ms = tot;
+  if (count) *count = (int64_t)ctx->evc_used;
+  if (reset) ctx->evc_used = 0;
   return SPX_OK;
 }
 

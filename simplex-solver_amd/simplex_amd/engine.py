@@ -308,6 +308,18 @@ class DeviceTableau:
         self._check(self._lib.spx_set_chain(self._ctx, int(mode), int(min_blocks)),
                     "spx_set_chain")
 
+    def set_chain_timing(self, on: bool = True) -> None:
+        """HIP events around every window's pivot chain (diagnostic)."""
+        self._check(self._lib.spx_set_chain_timing(self._ctx, 1 if on else 0),
+                    "spx_set_chain_timing")
+
+    def chain_timing(self, reset: bool = True):
+        """(total_ms, windows) of the event-timed pivot chains."""
+        ms, cnt = ctypes.c_double(), ctypes.c_int64()
+        self._check(self._lib.spx_chain_timing(self._ctx, ctypes.byref(ms), ctypes.byref(cnt),
+                                               1 if reset else 0), "spx_chain_timing")
+        return float(ms.value), int(cnt.value)
+
     def chain_blocks(self) -> int:
         """Blocks of the persistent chain for the loaded tableau (0: not used)."""
         b = ctypes.c_int()

@@ -162,3 +162,26 @@ def test_chain_set_validated(eng_cls):
             e.set_chain(4)
         with pytest.raises(Exception):
             e.set_chain(0, 300)
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+def test_chain_timing_events(eng_cls, mode):
+    """spx_set_chain_timing: one event pair per window (persistent or lazy
+    chain), same bytes as without the events."""
+    T, basis = _random_tableau(300, 700, seed=17)
+    with eng_cls(0) as e:
+        e.set_window(8)
+        e.set_chain(mode)
+        e.load(T, basis)
+        e.set_chain_timing(True)
+        e.run_pivots(40)
+        e.sync()
+        ms, n = e.chain_timing(reset=True)
+        assert n == 5 and ms > 0.0
+        e.set_chain_timing(False)
+        e.run_pivots(8)
+        e.sync()
+        assert e.chain_timing()[1] == 0
+        out, h = e.tableau(), e.history().tolist()
+    ref = _run(eng_cls, T, basis, 8, mode, max_iters=48)
+    assert h == ref[1] and out.tobytes() == ref[2].tobytes()
