@@ -318,14 +318,15 @@ __device__ __forceinline__ bool load_extras(const gu64* rec, int wb, int h0, int
   }
 }
 
-// Publish a block's record: wave w's winning lane has put its history (slots
-// 0..nh-1) and `extra` into hist_lds[w][], the wave keys are in sk[]; after the
-// block barrier wave 0 reduces the NW keys (every lane the same winner), its
-// lanes store the winner's extras, then lane 0 the header (program order: the
-// extras leave first).  RATIO: header v, row, t; extras [extra, history].
-template <int NW, bool RATIO>
+// Publish a block's record: the wave keys are in sk[], and hist(ww, idx, s)
+// returns slot s of the history of the winner idx of wave ww (s = 33: the
+// RATIO extra, the row's RHS); after the block barrier wave 0 reduces the NW
+// keys (every lane the same winner), its lanes store the winner's extras, then
+// lane 0 the header (program order: the extras leave first).  RATIO: header v,
+// row, t; extras [extra, history].
+template <int NW, bool RATIO, typename Hist>
 __device__ __forceinline__ void publish_record(gu64* rec, int b, unsigned tag, int nh,
-                                               const KeyP (&sk)[NW], const double (*hl)[34]) {
+                                               const KeyP (&sk)[NW], Hist hist) {
   const int lane = threadIdx.x & 63;
   KeyP k = sk[0];
 #pragma unroll
@@ -338,12 +339,13 @@ __device__ __forceinline__ void publish_record(gu64* rec, int b, unsigned tag, i
     // lane x < 2*nh: history granule x; RATIO: lanes 62, 63 the extra (row's RHS)
     if (lane < 2 * nh) {
       const unsigned long long x =
-          (unsigned long long)__double_as_longlong(hl[ww][lane >> 1]);
+          (unsigned long long)__double_as_longlong(hist(ww, k.row, lane >> 1));
       g_store(rb + (size_t)(H0 + lane) * CHAIN_MAX_BLOCKS, tag,
               (lane & 1) ? (unsigned)(x >> 32) : (unsigned)x);
     }
     if (RATIO && lane >= 62) {
-      const unsigned long long x = (unsigned long long)__double_as_longlong(hl[ww][33]);
+      const unsigned long long x =
+          (unsigned long long)__double_as_longlong(hist(ww, k.row, 33));
       g_store(rb + (size_t)(RATIO_HDR + (lane - 62)) * CHAIN_MAX_BLOCKS, tag,
               (lane & 1) ? (unsigned)(x >> 32) : (unsigned)x);
     }
@@ -378,13 +380,24 @@ __global__ __launch_bounds__(CB) void chain_kernel(
   static_assert(KMAX <= 32, "slots are lane-indexed and fit the window buffers");
   constexpr int NW = CB / 64;
   constexpr int CH = KMAX % 8 == 0 ? 8 : KMAX % 4 == 0 ? 4 : 2;
+  // LH: the window histories f_s[i] (rows) and p_s[j] (columns) live in LDS,
+  // slot-major, one column per thread: a phase reads its thread's slots once
+  // and appends one, instead of a 2*KMAX-select register update on the path
+  // to the record (and the winner's history is published straight from them)
+  constexpr bool LH = KMAX * CB * 16 <= 128 * 1024;
+  __shared__ double fsl[LH ? KMAX : 1][LH ? CB : 1];
+  __shared__ double psl[LH ? KMAX : 1][LH ? CB : 1];
+  __shared__ double hl33[NW];  // LH: the wave winners' RHS (the ratio record's extra)
   // one block per CU: the record protocol is validated for that residency
-  __shared__ double lds_pin[80 * 128];
+  // (with LH the histories already take most of it)
+  constexpr int PIN = LH ? (82 * 1024 - KMAX * CB * 16 > 8 ? (82 * 1024 - KMAX * CB * 16) / 8 : 1)
+                         : 80 * 128;
+  __shared__ double lds_pin[PIN];
   __shared__ int64_t bc_idx;  // the winner handed from wave 0 to the block
   __shared__ double bc_val;
   __shared__ int bc_blk;
   __shared__ KeyP sk[NW];       // the waves' best keys (payload b = wave index)
-  __shared__ double hl[NW][34];  // their winners' histories (+ [33]: the row's RHS)
+  __shared__ double hl[LH ? 1 : NW][34];  // their winners' histories (+ [33]: the row's RHS)
   gu64* gr_enter = (gu64*)gr_enter_;
   gu64* gr_ratio = (gu64*)gr_ratio_;
   const int B = gridDim.x;
@@ -424,7 +437,7 @@ __global__ __launch_bounds__(CB) void chain_kernel(
 #pragma unroll
   for (int s = 0; s < KMAX; ++s) fs[s] = ps[s] = 0.0;
   int64_t slot_r = 0, slot_c = -1;      // lane s: (r_s, c_s)
-  if (t == 0) lds_pin[b & 127] = 0.0;
+  if (t == 0) lds_pin[b % PIN] = 0.0;
   if (status0 != ST_RUNNING) {          // grid-uniform: no pivot in this window
     if (leader)
       for (int s = 0; s < npiv; ++s) win.made[s] = 0;  // (the flush counts made slots)
@@ -485,6 +498,10 @@ __global__ __launch_bounds__(CB) void chain_kernel(
     // column c on my row: stale + pending slots, in slot order; p_s[c] (lane
     // s) from the winning entering record's history
     double fv = A[c * ld + ic];
+    if constexpr (LH) {  // my row's f history, read while the gathers are in flight
+#pragma unroll
+      for (int s = 0; s < KMAX; ++s) fs[s] = fsl[s][t];
+    }
     double pcl = 0.0, unused[2];
     if (q > 0 &&
         !load_extras<0>(gr_enter, wb, ENTER_HDR, q, 0, rec_tag(W, q - 1, GK_ENTER), pcl, unused,
@@ -507,8 +524,12 @@ __global__ __launch_bounds__(CB) void chain_kernel(
       }
     }
     SPX_PROBE(q, 2, 1, fv != 12345.678);  // slots applied
+    if constexpr (LH) {
+      fsl[q][t] = fv;
+    } else {
 #pragma unroll
-    for (int s = 0; s < KMAX; ++s) fs[s] = (s == q) ? fv : fs[s];
+      for (int s = 0; s < KMAX; ++s) fs[s] = (s == q) ? fv : fs[s];
+    }
     f_prev = fv;
     KeyP k = keyp_none();
     if (ilive) {
@@ -524,15 +545,27 @@ __global__ __launch_bounds__(CB) void chain_kernel(
     // winner is published by wave 0 (rows grow with the lane: Dantzig's tie key)
     k = key_of_lane(k, wave_argmin(k.v, k.t, k.row >= 0, rule != RULE_BLAND));
     if (ilive && k.row == i) {
+      if constexpr (LH) {
+        hl33[w] = bcur;
+      } else {
 #pragma unroll
-      for (int s = 0; s < KMAX; ++s)
-        if (s <= q) hl[w][s] = fs[s];
-      hl[w][33] = bcur;
+        for (int s = 0; s < KMAX; ++s)
+          if (s <= q) hl[w][s] = fs[s];
+        hl[w][33] = bcur;
+      }
     }
     if (lane == 0) sk[w] = KeyP{k.v, k.t, k.row, 0.0, (double)w};
+    SPX_PROBE(q, 2, 2, k.v != 12345.678);  // wave argmin + LDS hand-off issued
     __syncthreads();
+    SPX_PROBE(q, 2, 3, true);              // every wave of the block arrived
     if (w0) {
-      publish_record<NW, true>(gr_ratio, b, rec_tag(W, q, GK_RATIO), q + 1, sk, hl);
+      publish_record<NW, true>(gr_ratio, b, rec_tag(W, q, GK_RATIO), q + 1, sk,
+                               [&](int ww, int64_t row, int x) -> double {
+                                 if constexpr (LH)
+                                   return x == 33 ? hl33[ww] : fsl[x][(int)(row - (int64_t)b * rpb)];
+                                 else
+                                   return hl[ww][x];
+                               });
       SPX_PROBE_CHAIN(q, 0);
     }
     // f_q for the flush / row_fix (later kernels): stored after the record, so
@@ -566,6 +599,10 @@ __global__ __launch_bounds__(CB) void chain_kernel(
     // row r on my column: stale + pending slots.  f_s[r] (lane s <= q, lane q
     // the pivot element) and the row's RHS from the winning ratio record
     double v = A[jc * ld + r];
+    if constexpr (LH) {  // my column's p history, read while the gathers are in flight
+#pragma unroll
+      for (int s = 0; s < KMAX; ++s) ps[s] = psl[s][t];
+    }
     double frl = 0.0, ex[2];
     if (!load_extras<1>(gr_ratio, wb, RATIO_HDR + 2, q + 1, RATIO_HDR, rec_tag(W, q, GK_RATIO),
                         frl, ex, st))
@@ -594,8 +631,10 @@ __global__ __launch_bounds__(CB) void chain_kernel(
     if (jlive) {
       const double p = v / piv;
       pq = p;
+      if constexpr (!LH) {
 #pragma unroll
-      for (int s = 0; s < KMAX; ++s) ps[s] = (s == q) ? p : ps[s];
+        for (int s = 0; s < KMAX; ++s) ps[s] = (s == q) ? p : ps[s];
+      }
       const bool nz = (p != 0.0) || !skip;
       if (j == c) {
         o = 0.0;
@@ -620,16 +659,26 @@ __global__ __launch_bounds__(CB) void chain_kernel(
     r_prev = r;
     SPX_PROBE(q, 1, 2, v != 12345.678);
     ek = key_of_lane(ek, wave_argmin(ek.v, ek.t, ek.row >= 0, true));  // columns grow with the lane
-    if (q + 1 < npiv && jlive && ek.row == j) {
+    if constexpr (LH) {
+      psl[q][t] = pq;
+    } else if (q + 1 < npiv && jlive && ek.row == j) {
 #pragma unroll
       for (int s = 0; s < KMAX; ++s)
         if (s <= q) hl[w][s] = ps[s];
     }
     if (lane == 0) sk[w] = KeyP{ek.v, ek.t, ek.row, ek.a, (double)w};
+    SPX_PROBE(q, 3, 2, ek.v != 12345.678);  // wave argmin + LDS hand-off issued
     __syncthreads();
+    SPX_PROBE(q, 3, 3, true);               // every wave of the block arrived
     if (w0) {
       if (q + 1 < npiv) {
-        publish_record<NW, false>(gr_enter, b, rec_tag(W, q, GK_ENTER), q + 1, sk, hl);
+        publish_record<NW, false>(gr_enter, b, rec_tag(W, q, GK_ENTER), q + 1, sk,
+                                  [&](int ww, int64_t col, int x) -> double {
+                                    if constexpr (LH)
+                                      return psl[x][(int)(col - (int64_t)b * cpb)];
+                                    else
+                                      return hl[ww][x];
+                                  });
       } else if (t == 0) {
         // the next window's pivot-0 partial (read after the kernel boundary)
         KeyP kb = sk[0];
@@ -693,7 +742,7 @@ __global__ __launch_bounds__(CB) void chain_kernel(
     reinterpret_cast<int64_t*>(rc_)[0] = j | ((int64_t)(tg >> 30) << 32);
 #pragma unroll
     for (int s = 0; s < KMAX; ++s)
-      if (s < q) rc_[2 + s] = ps[s];
+      if (s < q) rc_[2 + s] = LH ? psl[s][t] : ps[s];
   }
 }
 

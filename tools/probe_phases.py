@@ -76,8 +76,10 @@ def main():
             prev_end = ph[3]
             if a.chain != 1 and t(q, 2 + kind, 0) > t0:
                 a0, a1 = us(t(q, 2 + kind, 0)), us(t(q, 2 + kind, 1))
+                a2, a3 = us(t(q, 2 + kind, 2)), us(t(q, 2 + kind, 3))
                 print(f"       fine: loads arrived +{a0 - ph[1]:5.2f}  slots applied "
-                      f"+{a1 - a0:5.2f}  rest of phase2 +{ph[2] - a1:5.2f}")
+                      f"+{a1 - a0:5.2f}  rest of phase2 +{ph[2] - a1:5.2f}  | end: argmin+lds "
+                      f"+{a2 - ph[2]:5.2f}  barrier +{a3 - a2:5.2f}  publish +{ph[3] - a3:5.2f}")
             if kind == 0 and os.environ.get("SPX_PROBE_FINE"):
                 k0, k1 = us(t(q, 2, 0)), us(t(q, 2, 1))
                 print(f"       fine: keys reduced +{k0 - ph[0]:5.2f}  wave_min +{k1 - k0:5.2f}")
