@@ -437,6 +437,9 @@ __global__ __launch_bounds__(CB) void chain_kernel(
 #pragma unroll
   for (int s = 0; s < KMAX; ++s) fs[s] = ps[s] = 0.0;
   int64_t slot_r = 0, slot_c = -1;      // lane s: (r_s, c_s)
+  // per-thread slot masks (bit s): my row left at slot s (i == r_s), my column
+  // entered at slot s (j == c_s), p_s[j] == 0 under the skip rule
+  uint32_t rmask = 0u, cmask = 0u, zmask = 0u;
   if (t == 0) lds_pin[b % PIN] = 0.0;
   if (status0 != ST_RUNNING) {          // grid-uniform: no pivot in this window
     if (leader)
@@ -510,16 +513,51 @@ __global__ __launch_bounds__(CB) void chain_kernel(
     SPX_PROBE(q, 2, 0, fv != 12345.678 && pcl != 12345.678);  // loads arrived
     // RHS: apply slot q-1 (the slots before it are already in bcur)
     if (q > 0) bcur = apply_sel(bcur, i == r_prev, false, true, f_prev, prhs, skip);
+    // apply_sel's special cases as masks: column c entered earlier in this
+    // window or p_s[c] == 0 under the skip rule (uniform: the exact loop), my
+    // row left at slot s (rmask: p_s[c] replaces the msub on that lane).
+    // Otherwise a slot is one msub (~5 VALU ops instead of ~25).
+    const uint32_t qm = (1u << q) - 1u;
+    if (__ballot(lane < q && (slot_c == c || (skip && pcl == 0.0))) == 0ull) {
+      if (__ballot((rmask & qm) != 0u) == 0ull) {
 #pragma unroll
-    for (int c8 = 0; c8 < KMAX; c8 += CH) {
-      if (c8 < q) {
+        for (int c8 = 0; c8 < KMAX; c8 += CH) {
+          if (c8 < q) {
 #pragma unroll
-        for (int u = 0; u < CH; ++u) {
-          const int s = c8 + u;
-          const bool act = s < q;
-          const bool isr = i == rdlane64(slot_r, s);
-          const bool isc = c == rdlane64(slot_c, s);
-          fv = apply_sel(fv, isr, isc, act, fs[s], rdlane(pcl, s), skip);
+            for (int u = 0; u < CH; ++u) {
+              const int s = c8 + u;
+              const double x = msub(fv, fs[s], rdlane(pcl, s));
+              fv = s < q ? x : fv;
+            }
+          }
+        }
+      } else {
+#pragma unroll
+        for (int c8 = 0; c8 < KMAX; c8 += CH) {
+          if (c8 < q) {
+#pragma unroll
+            for (int u = 0; u < CH; ++u) {
+              const int s = c8 + u;
+              const double p_s = rdlane(pcl, s);
+              double x = msub(fv, fs[s], p_s);
+              x = ((rmask >> s) & 1u) ? p_s : x;
+              fv = s < q ? x : fv;
+            }
+          }
+        }
+      }
+    } else {
+#pragma unroll
+      for (int c8 = 0; c8 < KMAX; c8 += CH) {
+        if (c8 < q) {
+#pragma unroll
+          for (int u = 0; u < CH; ++u) {
+            const int s = c8 + u;
+            const bool act = s < q;
+            const bool isr = i == rdlane64(slot_r, s);
+            const bool isc = c == rdlane64(slot_c, s);
+            fv = apply_sel(fv, isr, isc, act, fs[s], rdlane(pcl, s), skip);
+          }
         }
       }
     }
@@ -610,18 +648,51 @@ __global__ __launch_bounds__(CB) void chain_kernel(
     SPX_PROBE(q, 3, 0, v != 12345.678 && frl != 12345.678);  // loads arrived
     const double piv = rdlane(frl, q);
     prhs = ex[0] / piv;  // p_q[rhs]: lazy_norm's p = v / piv of the RHS column
-    bool zb = false;
+    // Special cases as masks: row r left earlier in the window (uniform: the
+    // exact loop), my column entered at slot s (cmask: the value becomes 0),
+    // p_s[j] == 0 under the skip rule (zmask: the value is kept)
+    const uint32_t qmn = (1u << q) - 1u;
+    const bool zb = (zmask & qmn) != 0u;
+    if (__ballot(lane < q && slot_r == r) == 0ull) {
+      if (__ballot(jlive && ((zmask | cmask) & qmn) != 0u) == 0ull) {
 #pragma unroll
-    for (int c8 = 0; c8 < KMAX; c8 += CH) {
-      if (c8 < q) {
+        for (int c8 = 0; c8 < KMAX; c8 += CH) {
+          if (c8 < q) {
 #pragma unroll
-        for (int u = 0; u < CH; ++u) {
-          const int s = c8 + u;
-          const bool act = s < q;
-          const bool isr = r == rdlane64(slot_r, s);
-          const bool isc = jc == rdlane64(slot_c, s);
-          v = apply_sel(v, isr, isc, act, rdlane(frl, s), ps[s], skip);
-          zb |= act && skip && ps[s] == 0.0;
+            for (int u = 0; u < CH; ++u) {
+              const int s = c8 + u;
+              const double x = msub(v, rdlane(frl, s), ps[s]);
+              v = s < q ? x : v;
+            }
+          }
+        }
+      } else {
+#pragma unroll
+        for (int c8 = 0; c8 < KMAX; c8 += CH) {
+          if (c8 < q) {
+#pragma unroll
+            for (int u = 0; u < CH; ++u) {
+              const int s = c8 + u;
+              double x = msub(v, rdlane(frl, s), ps[s]);
+              x = ((zmask >> s) & 1u) ? v : x;
+              x = ((cmask >> s) & 1u) ? 0.0 : x;
+              v = s < q ? x : v;
+            }
+          }
+        }
+      }
+    } else {
+#pragma unroll
+      for (int c8 = 0; c8 < KMAX; c8 += CH) {
+        if (c8 < q) {
+#pragma unroll
+          for (int u = 0; u < CH; ++u) {
+            const int s = c8 + u;
+            const bool act = s < q;
+            const bool isr = r == rdlane64(slot_r, s);
+            const bool isc = jc == rdlane64(slot_c, s);
+            v = apply_sel(v, isr, isc, act, rdlane(frl, s), ps[s], skip);
+          }
         }
       }
     }
@@ -631,6 +702,8 @@ __global__ __launch_bounds__(CB) void chain_kernel(
     if (jlive) {
       const double p = v / piv;
       pq = p;
+      zmask |= (skip && p == 0.0) ? (1u << q) : 0u;
+      cmask |= (j == c) ? (1u << q) : 0u;
       if constexpr (!LH) {
 #pragma unroll
         for (int s = 0; s < KMAX; ++s) ps[s] = (s == q) ? p : ps[s];
@@ -652,6 +725,7 @@ __global__ __launch_bounds__(CB) void chain_kernel(
       if (j < n_enter && o < -eps_opt) kmin2(ek, rule == RULE_BLAND ? 0.0 : o, j, j, o, 0.0);
     }
     if (ilive && i == r) bas = c;
+    rmask |= (i == r) ? (1u << q) : 0u;
     if (lane == q) {
       slot_r = r;
       slot_c = c;
