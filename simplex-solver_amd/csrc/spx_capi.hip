@@ -422,6 +422,10 @@ int enqueue_window_t(spx_ctx* ctx, int npiv, bool time_flush) {
   const int nbw = lazy_ratio_grid(ctx);
   int cb = BLK;
   const int B = chain_blocks(ctx, &cb);
+  // the register-ring flush variants read p_s[j] from P; the LDS-DMA flush
+  // and row_fix read the window's records
+  constexpr bool POW2K = (KMAX & (KMAX - 1)) == 0;
+  const bool reg_ring_flush = POW2K && ctx->flush_var >= 1 && ctx->flush_var <= 5;
   std::pair<hipEvent_t, hipEvent_t>* ec = nullptr;
   if (ctx->time_chain) {
     int rc = next_event_pair(ctx, ctx->evc, ctx->evc_used, &ec);
@@ -435,7 +439,8 @@ int enqueue_window_t(spx_ctx* ctx, int npiv, bool time_flush) {
     hipLaunchKernelGGL(kern, dim3(B), dim3(cb), 0, ctx->stream, ctx->enter_part, ctx->st,
                        (const Params*)ctx->prm, std::max(NWAVE * ctx->nbn, B),
                        (const double*)ctx->A, ctx->ld, ctx->m_local, ctx->N, ctx->obj, ctx->win,
-                       npiv, ctx->basis, ctx->hist, ctx->gr_enter, ctx->gr_ratio, cpb, rpb);
+                       npiv, ctx->basis, ctx->hist, ctx->gr_enter, ctx->gr_ratio, cpb, rpb,
+                       reg_ring_flush ? 1 : 0);
   }
   for (int q = 0; B == 0 && q < npiv; ++q) {
     hipLaunchKernelGGL(lazy_ratio_kernel<KMAX>, dim3(nbw), dim3(BLK), 0, ctx->stream,

@@ -376,7 +376,7 @@ __global__ __launch_bounds__(CB) void chain_kernel(
     Key* __restrict__ enter_part, State* st, const Params* __restrict__ prm, int n_ep,
     const double* __restrict__ A, int64_t ld, int64_t m, int64_t N, double* __restrict__ obj,
     Window win, int npiv, int64_t* __restrict__ basis, int64_t* __restrict__ hist,
-    unsigned long long* gr_enter_, unsigned long long* gr_ratio_, int cpb, int rpb) {
+    unsigned long long* gr_enter_, unsigned long long* gr_ratio_, int cpb, int rpb, int wp) {
   static_assert(KMAX <= 32, "slots are lane-indexed and fit the window buffers");
   constexpr int NW = CB / 64;
   constexpr int CH = KMAX % 8 == 0 ? 8 : KMAX % 4 == 0 ? 4 : 2;
@@ -763,8 +763,9 @@ __global__ __launch_bounds__(CB) void chain_kernel(
       SPX_PROBE_CHAIN(q, 2);
     }
     // stores for later kernels, after the record (never queued in front of it):
-    // p_q for row_fix, the pivot's bookkeeping
-    if (jlive) win.P[j * KW + q] = pq;
+    // p_q for the register-ring flush variants (wp; the LDS-DMA flush and
+    // row_fix read the records), the pivot's bookkeeping
+    if (wp && jlive) win.P[j * KW + q] = pq;
     if (leader) {
       st->r = r;
       st->c = c;

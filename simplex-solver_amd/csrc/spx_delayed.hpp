@@ -1250,7 +1250,8 @@ __global__ __launch_bounds__(BLK + 64) void flush_dyn_kernel(double* __restrict_
 
 // ---------------------------------------------------------------------------
 // row_fix_kernel<K>: after a window's flush (its made slots: a prefix of K),
-// rewrite the leaving rows of the fast-path columns (tagged, not SPECIAL / ZERO).  For such a column no
+// rewrite the leaving rows of the fast-path columns (the window's records
+// without SPECIAL / ZERO flags; p values from the records).  For such a column no
 // pivot of the window enters it and every p_s[j] != 0, so a leaving row r
 // whose last leaving slot is L ends at p_L[j] followed by the later pivots'
 // msub updates (their leaving rows differ from r).  One thread per column.
@@ -1259,6 +1260,7 @@ template <int K>
 __global__ __launch_bounds__(BLK) void row_fix_kernel(double* __restrict__ A, int64_t ld,
                                                       int64_t m_local, int64_t row0, int64_t N,
                                                       Window win, int npiv) {
+  (void)N;
   __shared__ double fr[K][K];  // fr[L][s] = f_s[r_L]
   __shared__ int64_t rows[K];
   __shared__ int lastL[K];
@@ -1266,18 +1268,20 @@ __global__ __launch_bounds__(BLK) void row_fix_kernel(double* __restrict__ A, in
   // follows every flush on the stream)
   if (blockIdx.x == 0)
     for (int t = threadIdx.x; t < win.nclaim; t += BLK) win.claim[t] = 0u;
-  // all loads are independent: issue them together
-  const int64_t j = (int64_t)blockIdx.x * BLK + threadIdx.x;
-  const bool live = j < N;
-  const uint32_t tg = live ? win.tag[j] : 0u;
-  const uint32_t epoch = *win.epoch & TAG_EPOCH;
+  // one thread per record of the window (the flush's compacted list: column,
+  // path flags, p_0..p_{K-1}); all loads are independent: issue them together
+  const int kr = blockIdx.x * BLK + threadIdx.x;
+  const bool live = kr < *win.nlist;
+  const int64_t hdr = reinterpret_cast<const int64_t*>(win.rec)[(int64_t)(live ? kr : 0) * RECW];
+  const int64_t j = hdr & 0xffffffffll;
+  const bool fast = (hdr >> 32) == 0;  // not SPECIAL / ZERO: the flush's plain msub chain
   int madeK = 0;  // made slots of this window: a prefix of its npiv launched ones
   for (int s = 0; s < npiv; ++s) madeK += win.made[s];
   double p[K];
 #pragma unroll
-  for (int s = 0; s < K; ++s) p[s] = win.P[(live ? j : 0) * KW + s];
+  for (int s = 0; s < K; ++s) p[s] = win.rec[(int64_t)(live ? kr : 0) * RECW + 2 + s];
   // (loaded before the made-count check: a slot not made in this window holds a
-  // stale row, so the index is clamped; such values are never used)
+  // stale value, so the index is clamped; such values are never used)
   for (int x = threadIdx.x; x < K * K; x += BLK) {
     const int L = x / K, s = x % K;
     const int64_t rl = min(max(win.r[L] - row0, (int64_t)0), m_local - 1);
@@ -1291,8 +1295,7 @@ __global__ __launch_bounds__(BLK) void row_fix_kernel(double* __restrict__ A, in
     lastL[threadIdx.x] = last;
   }
   __syncthreads();
-  if (madeK == 0 || !live || (tg & TAG_EPOCH) != epoch || (tg & (TAG_SPECIAL | TAG_ZERO)))
-    return;
+  if (madeK == 0 || !live || !fast) return;
 #pragma unroll
   for (int L = 0; L < K; ++L) {
     if (L >= madeK || !lastL[L] || rows[L] < 0 || rows[L] >= m_local) continue;  // not ours
