@@ -66,7 +66,8 @@ def parse():
                          "-1 = default: %d, on one GPU and on row shards)" % DEFAULT_WINDOW)
     ap.add_argument("--chain", type=int, default=0,
                     help="window pivot chain: 0 one persistent launch per window (default, "
-                         "single GPU), 1 two launches per pivot")
+                         "single GPU), 1 two launches per pivot, 2 / 3 persistent with 256- / "
+                         "512-thread blocks")
     ap.add_argument("--chain-blocks", type=int, default=0, help="persistent chain grid (0: minimum)")
     ap.add_argument("--time-every", type=int, default=0,
                     help="HIP events around every k-th elimination (or window flush) of the "

@@ -130,8 +130,8 @@ struct spx_ctx {
   int win_k = 0;
   Window win{};
   // persistent pivot chain of a window (spx_chain.hpp): record buffers and mode
-  unsigned long long* gr_enter = nullptr;  // ENTER_REC x CHAIN_MAX_BLOCKS granules
-  unsigned long long* gr_ratio = nullptr;  // RATIO_REC x CHAIN_MAX_BLOCKS granules
+  unsigned long long* gr_enter = nullptr;  // CHAIN_REC granules (spx_chain.hpp layout)
+  unsigned long long* gr_ratio = nullptr;  // CHAIN_REC granules
   int chain_mode = 0;      // 0: persistent chain when it fits, 1: launch per phase
   int chain_min_blocks = 0;
 
@@ -398,7 +398,9 @@ int chain_blocks(spx_ctx* ctx, int* cb_out = nullptr) {
   const int cb = ctx->chain_mode == 2 ? 256 : ctx->chain_mode == 3 ? 512
                  : (wide > 256 * std::min(ctx->n_cu, CHAIN_MAX_BLOCKS) ? 512 : 256);
   if (cb_out) *cb_out = cb;
-  const int64_t need = std::max<int64_t>({(ctx->N + cb - 1) / cb, (ctx->m_local + cb - 1) / cb,
+  // the N-1 candidate columns set the width: the RHS column rides along with
+  // the last block's last thread when B * cpb == N - 1 (spx_chain.hpp, xown)
+  const int64_t need = std::max<int64_t>({(ctx->N - 1 + cb - 1) / cb, (ctx->m_local + cb - 1) / cb,
                                           1, (int64_t)ctx->chain_min_blocks});
   const int64_t cap = std::min<int64_t>((int64_t)ctx->n_cu, CHAIN_MAX_BLOCKS);
   return need <= cap ? (int)need : 0;
@@ -433,7 +435,7 @@ int enqueue_window_t(spx_ctx* ctx, int npiv, bool time_flush) {
     if (rc) return rc;
   }
   if (B > 0) {
-    const int cpb = (int)((ctx->N + B - 1) / B);
+    const int cpb = (int)((ctx->N - 1 + B - 1) / B);  // (B * cpb == N-1: xown owns the RHS)
     const int rpb = (int)((ctx->m_local + B - 1) / B);
     auto kern = cb == 512 ? chain_kernel<KMAX, 512> : chain_kernel<KMAX, 256>;
     hipLaunchKernelGGL(kern, dim3(B), dim3(cb), 0, ctx->stream, ctx->enter_part, ctx->st,

@@ -431,6 +431,17 @@ __global__ __launch_bounds__(CB) void chain_kernel(
   double o = obj[jc];
   uint32_t tg = jlive ? win.tag[jc] : 0u;
   const uint32_t tg0 = tg;
+  // The RHS column N-1 is never an entering candidate and its pivot-row value
+  // is the ratio record's p_q[rhs] (the row owner's current RHS / pivot), so
+  // when the host sizes the grid by the N-1 candidate columns (B * cpb == N-1:
+  // 64 blocks at config 3, a single-pass poll) the last thread of the last
+  // block keeps it beside its own column: objective value, tag, p history.
+  const bool xown = (int64_t)B * cpb == N - 1 && b == B - 1 && t == CB - 1;
+  double ox = xown ? obj[N - 1] : 0.0;
+  uint32_t tgx = xown ? win.tag[N - 1] : 0u;
+  const uint32_t tgx0 = tgx;
+  uint32_t zmx = 0u;
+  __shared__ double pxl[KMAX];  // p_s[N-1] (xown only)
   double bcur = A[(N - 1) * ld + ic];   // current RHS of my row (stale + applied slots)
   int64_t bas = basis[ic];              // basis[i] (Bland's tie key)
   double fs[KMAX], ps[KMAX];            // f_s[i], p_s[j] of this window
@@ -724,6 +735,20 @@ __global__ __launch_bounds__(CB) void chain_kernel(
       // key (o, j) under Dantzig, (0, j) under Bland; payload o (z_c)
       if (j < n_enter && o < -eps_opt) kmin2(ek, rule == RULE_BLAND ? 0.0 : o, j, j, o, 0.0);
     }
+    if (xown) {  // the RHS column: the same update with p = p_q[rhs] (never j == c)
+      const bool zbx = (zmx & qmn) != 0u;
+      zmx |= (skip && prhs == 0.0) ? (1u << q) : 0u;
+      const bool nz = (prhs != 0.0) || !skip;
+      if (nz) ox = msub(ox, zc, prhs);
+      const bool tagged = (tgx & TAG_EPOCH) == W;
+      if (nz) {
+        tgx = W | ((tagged && (tgx & TAG_SPECIAL)) ? TAG_SPECIAL : 0u) | (zbx ? TAG_ZERO : 0u);
+      } else if (tagged) {
+        tgx = tgx | TAG_ZERO;
+      }
+      pxl[q] = prhs;
+      if (wp) win.P[(N - 1) * KW + q] = prhs;
+    }
     if (ilive && i == r) bas = c;
     rmask |= (i == r) ? (1u << q) : 0u;
     if (lane == q) {
@@ -793,14 +818,21 @@ __global__ __launch_bounds__(CB) void chain_kernel(
     obj[j] = o;
     if (tg != tg0) win.tag[j] = tg;
   }
+  if (xown) {
+    obj[N - 1] = ox;
+    if (tgx != tgx0) win.tag[N - 1] = tgx;
+  }
   if (q == 0) return;  // no pivot made: nothing to compact (the flush sees nm == 0)
   // compact the window's touched columns into records for the flush (as
-  // lazy_norm's last slot): wave ballot + LDS prefix + one atomic per block
+  // lazy_norm's last slot): wave ballot + LDS prefix + one atomic per block;
+  // the RHS column (xown) follows its wave's own columns
   const bool mine = jlive && (tg & TAG_EPOCH) == W;
+  const bool minex = xown && (tgx & TAG_EPOCH) == W;
   __shared__ int wcnt[NW];
   __shared__ int base;
   const uint64_t bal = __ballot(mine);
-  if (lane == 0) wcnt[w] = __popcll(bal);
+  const uint64_t balx = __ballot(minex);
+  if (lane == 0) wcnt[w] = __popcll(bal) + __popcll(balx);
   __syncthreads();
   if (t == 0) {
     int tot = 0;
@@ -818,6 +850,16 @@ __global__ __launch_bounds__(CB) void chain_kernel(
 #pragma unroll
     for (int s = 0; s < KMAX; ++s)
       if (s < q) rc_[2 + s] = LH ? psl[s][t] : ps[s];
+  }
+  if (minex) {
+    const int px = pos - __popcll(bal & ((1ull << lane) - 1ull)) + __popcll(bal);
+    if (px < N) {
+      double* rc_ = win.rec + (int64_t)px * RECW;
+      reinterpret_cast<int64_t*>(rc_)[0] = (N - 1) | ((int64_t)(tgx >> 30) << 32);
+#pragma unroll
+      for (int s = 0; s < KMAX; ++s)
+        if (s < q) rc_[2 + s] = pxl[s];
+    }
   }
 }
 

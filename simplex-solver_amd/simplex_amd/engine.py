@@ -303,7 +303,8 @@ class DeviceTableau:
 
     def set_chain(self, mode: int = 0, min_blocks: int = 0) -> None:
         """Pivot chain of a window: 0 = one persistent launch per window when
-        the tableau fits (default), 1 = two launches per pivot (lazy kernels).
+        the tableau fits (default), 1 = two launches per pivot (lazy kernels),
+        2 / 3 = persistent with 256- / 512-thread blocks.
         Bit-identical either way; min_blocks raises the persistent grid."""
         self._check(self._lib.spx_set_chain(self._ctx, int(mode), int(min_blocks)),
                     "spx_set_chain")

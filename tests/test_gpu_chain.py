@@ -62,12 +62,13 @@ def test_chain_matches_lazy_chain_and_oracle(eng_cls, K, shape, rule, mode):
     assert np.array_equal(out, ref) and np.array_equal(b, rb)
 
 
+@pytest.mark.parametrize("mode", [0])
 @pytest.mark.parametrize("min_blocks", [0, 3, 64, 100, 256])
-def test_chain_grid_sizes_bit_exact(eng_cls, min_blocks):
+def test_chain_grid_sizes_bit_exact(eng_cls, min_blocks, mode):
     """More blocks than the minimum (fewer columns / rows per block, more than
     64 records per poll) give the same bytes."""
     T, basis = _random_tableau(400, 1300, seed=11 + min_blocks)
-    res, h, out, b, blocks = _run(eng_cls, T, basis, 16, 0, min_blocks, max_iters=53)
+    res, h, out, b, blocks = _run(eng_cls, T, basis, 16, mode, min_blocks, max_iters=53)
     res1, h1, out1, b1, _ = _run(eng_cls, T, basis, 16, 1, max_iters=53)
     assert blocks == max(min_blocks, 6)
     assert h == h1 and res.iters == res1.iters and out.tobytes() == out1.tobytes()
@@ -84,11 +85,30 @@ def test_chain_wide_tableau_more_than_64_blocks(eng_cls, mode, nb):
     assert h == h1 and out.tobytes() == out1.tobytes() and np.array_equal(b, b1)
 
 
+@pytest.mark.parametrize("K", [8, 24])
+@pytest.mark.parametrize("mode,nb", [(0, 64), (2, 64), (3, 32)])
+def test_chain_config3_width_rhs_column_rides_along(eng_cls, K, mode, nb):
+    """Config 3's width: N - 1 = 16384 candidate columns = 64 x 256, so the
+    grid is 64 blocks (one record per polling lane) and the RHS column is kept
+    by the last thread of the last block (spx_chain.hpp, xown): objective
+    value, tag, p history and its flush record must match the lazy chain."""
+    T, basis = _random_tableau(301, 16385, seed=8 + K)
+    res, h, out, b, blocks = _run(eng_cls, T, basis, K, mode, max_iters=3 * K + 1)
+    assert blocks == nb
+    res1, h1, out1, b1, _ = _run(eng_cls, T, basis, K, 1, max_iters=3 * K + 1)
+    assert h == h1 and res.status == res1.status and res.iters == res1.iters
+    assert out.tobytes() == out1.tobytes() and np.array_equal(b, b1)
+    ref, rb = T.copy(), basis.copy()
+    st, hist = O.solve_tableau(ref, rb, max_iters=3 * K + 1)
+    assert [tuple(x) for x in h] == hist and np.array_equal(out, ref)
+
+
 @pytest.mark.parametrize("K", [4, 32])
-def test_chain_degenerate_bland_full_solve(eng_cls, K):
+@pytest.mark.parametrize("mode", [0, 3])
+def test_chain_degenerate_bland_full_solve(eng_cls, K, mode):
     from simplex_amd import synth
     T, basis = synth.full_tableau("degenerate", 96, 96, seed=3)
-    res, h, out, b, _ = _run(eng_cls, T, basis, K, 0, rule="bland")
+    res, h, out, b, _ = _run(eng_cls, T, basis, K, mode, rule="bland")
     res1, h1, out1, b1, _ = _run(eng_cls, T, basis, K, 1, rule="bland")
     ref, rb = T.copy(), basis.copy()
     st, hist = O.solve_tableau(ref, rb, rule="bland")
