@@ -328,9 +328,19 @@ template <int NW, bool RATIO, typename Hist>
 __device__ __forceinline__ void publish_record(gu64* rec, int b, unsigned tag, int nh,
                                                const KeyP (&sk)[NW], Hist hist) {
   const int lane = threadIdx.x & 63;
-  KeyP k = sk[0];
+  KeyP k;
+  if constexpr (NW == 4) {
+    // one LDS read (lane x < 4 takes wave x's key) and two quad DPP steps,
+    // instead of four dependent broadcast reads and compares
+    k = lane < NW ? sk[lane] : keyp_none();
+    kmin2_dpp<0xB1>(k);  // quad_perm [1,0,3,2]
+    kmin2_dpp<0x4E>(k);  // quad_perm [2,3,0,1]
+    k = key_of_lane(k, 0);
+  } else {
+    k = sk[0];
 #pragma unroll
-  for (int x = 1; x < NW; ++x) kmin2(k, sk[x].v, sk[x].t, sk[x].row, sk[x].a, sk[x].b);
+    for (int x = 1; x < NW; ++x) kmin2(k, sk[x].v, sk[x].t, sk[x].row, sk[x].a, sk[x].b);
+  }
   const int ww = (int)k.b;  // the winning wave (a payload slot of the block key)
   const bool none = k.row < 0;
   gu64* rb = rec + b;

@@ -2,7 +2,8 @@
 # A/B sweep of bench.py configurations, interleaved over ROUNDS rounds, one
 # bench process per configuration.  CONFIGS: ';'-separated bench argument
 # lists, each optionally prefixed "NAME|" to run with
-# simplex_amd/lib/libspx_NAME.so (same-box A/B of two builds).  Output:
+# simplex_amd/lib/libspx_NAME.so (same-box A/B of two builds) or, as
+# "env:VAR=VALUE|", with that environment variable set.  Output:
 # gpurun_out/$OUT/sweep.jsonl (value + flush time per run).
 set -u
 cd "${GRAFT_REPO_ROOT}"
@@ -12,10 +13,12 @@ mkdir -p "$O"
 IFS=';' read -ra CF <<< "${CONFIGS}"
 for r in $(seq 1 "${ROUNDS:-2}"); do
   for cfg in "${CF[@]}"; do
-    lib=""; c="$cfg"
+    lib=""; c="$cfg"; envs=""
     if [[ "$cfg" == *"|"* ]]; then lib="${cfg%%|*}"; c="${cfg#*|}"; fi
+    # "env:VAR=VALUE|args": run with that environment variable instead of another library
+    if [[ "$lib" == env:* ]]; then envs="${lib#env:}"; lib=""; fi
     if [ -n "$lib" ]; then export SPX_LIB="$PWD/simplex-solver_amd/simplex_amd/lib/libspx_$lib.so"; else unset SPX_LIB; fi
-    timeout -k 10 200 python bench.py --cpu-seconds 0 ${STEPS:---steps 40 --warmup 5} $c > "$O/last.log" 2>&1
+    env $envs timeout -k 10 200 python bench.py --cpu-seconds 0 ${STEPS:---steps 40 --warmup 5} $c > "$O/last.log" 2>&1
     rc=$?
     if [ $rc != 0 ]; then echo "config [$c] rc=$rc"; tail -5 "$O/last.log"; exit $rc; fi
     python - "$cfg" "$r" "$O/last.log" >> "$O/sweep.jsonl" <<'EOF'
