@@ -22,6 +22,7 @@
 #include <chrono>
 #include <condition_variable>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <mutex>
@@ -119,6 +120,7 @@ struct spx_ctx {
   std::map<const void*, int> flush_bpc;
   int flush_var = 0;       // flush kernel variant (rows per thread x columns per step)
   int flush_map = 0;       // flush block -> (row chunk, column group) map
+  int flush_tail = FLUSH_TAIL_DEFAULT;  // % of the records rows moved to the tail (spx_delayed.hpp)
   int last_flush_G = 0;    // column groups of the last flush launch
   int last_flush_rch = 0;  // row chunks of the last flush launch
   int n_cu = 0;
@@ -491,7 +493,7 @@ int enqueue_window_t(spx_ctx* ctx, int npiv, bool time_flush) {
     ctx->last_flush_rch = rch;
     hipLaunchKernelGGL(kern, dim3(rch * G), dim3(threads), 0, ctx->stream, ctx->A, ctx->ld,
                        ctx->m_local, ctx->row0, ctx->N, ctx->win, npiv, rch, G, ctx->prm,
-                       ctx->st, ctx->flush_map);
+                       ctx->st, ctx->flush_map | ctx->flush_tail << 8);
   };
   const bool nts = (ctx->elim_nt & 2) != 0;
   // variants: 0 (default) LDS-DMA ring of 12 columns per wave over the
@@ -803,6 +805,9 @@ int spx_create(spx_ctx** out, int device) {
     return SPX_E_HIP;
   }
   std::memset(ctx->h_st, 0, sizeof(State));
+  // tuning hook: SPX_FLUSH_TAIL=x (0..50) overrides the flush's tail share
+  if (const char* ft = std::getenv("SPX_FLUSH_TAIL"))
+    ctx->flush_tail = std::max(0, std::min(50, std::atoi(ft)));
   *out = ctx;
   return SPX_OK;
 }

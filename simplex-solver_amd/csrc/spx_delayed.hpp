@@ -837,6 +837,17 @@ __device__ __forceinline__ void wait_vmcnt() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
+// Record split of flush_lds_kernel: group g takes records g, g+G, g+2G, ...
+// (rows of G records, streamed side by side).  A CU's three flush blocks are
+// dispatched in three rounds (group-major map: round = 3g / G), and the
+// hardware issues from the oldest wave first, so with equal shares the
+// third-round blocks ended last and streamed alone
+// (profiles/r02/phases_flush_prio.log).  With a tail share x % (fmap bits
+// 8-15), the last x % of the record rows go to the first two rounds' groups
+// only, still strided: group g takes rows 0..M-1 as before, then (g < Gt =
+// 2G/3) records M*G + g, M*G + g + Gt, ...
+constexpr int FLUSH_TAIL_DEFAULT = 12;  // profiles/r02/ab/flush_tail_split_ab.jsonl
+
 template <int K, int D, bool NTS, bool PART = false>
 __global__ __launch_bounds__(BLK) void flush_lds_kernel(double* __restrict__ A, int64_t ld,
                                                         int64_t m_local, int64_t row0,
@@ -869,8 +880,16 @@ __global__ __launch_bounds__(BLK) void flush_lds_kernel(double* __restrict__ A, 
     st->iters += nm;
   }
   const int64_t wrow = (int64_t)chunk * 2 * BLK + (int64_t)w * 128;  // this wave's first row
-  if (wrow >= m_local || g >= L) return;  // wave-uniform: nothing to do
-  const int cnt = (L - g + G - 1) / G;    // this wave's records: g, g+G, ...
+  // this wave's records: g, g+G, ... for rows k < M, then the tail (see above)
+  const int tailp = (fmap & 3) == 0 ? (fmap >> 8) & 0xff : 0;
+  const int Gt = tailp ? max(1, 2 * G / 3) : G;
+  const int M = tailp ? (int)((int64_t)(L / G) * (100 - tailp) / 100) : 0x7fffffff;
+  int cnt = g < L ? (L - g + G - 1) / G : 0;
+  if (tailp) {
+    const int tl = L - M * G;  // tail records, strided over groups 0..Gt-1
+    cnt = M + (g < Gt && g < tl ? (tl - g + Gt - 1) / Gt : 0);
+  }
+  if (wrow >= m_local || cnt <= 0) return;  // wave-uniform: nothing to do
   const int64_t i0 = wrow + 2 * lane;
   const bool ok = i0 < m_local;            // the pair (i0, i0+1) holds local rows
   const int64_t i0c = ok ? i0 : wrow;      // in-column address for idle lanes
@@ -891,7 +910,9 @@ __global__ __launch_bounds__(BLK) void flush_lds_kernel(double* __restrict__ A, 
   ci64* hdr = (ci64*)win.rec;
   ci64* wr = (ci64*)win.r;
   ci64* wc = (ci64*)win.c;
-  auto rec_of = [&](int k) -> int64_t { return (int64_t)(g + (int64_t)k * G) * RECW; };
+  auto rec_of = [&](int k) -> int64_t {
+    return (k < M ? g + (int64_t)k * G : (int64_t)M * G + g + (int64_t)(k - M) * Gt) * RECW;
+  };
   const uint32_t lds0 =
       (uint32_t)(uintptr_t)((__attribute__((address_space(3))) dbl2*)&ring[0]) +
       (uint32_t)(w * D * 64) * (uint32_t)sizeof(dbl2);
