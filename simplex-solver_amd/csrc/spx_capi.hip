@@ -132,8 +132,8 @@ struct spx_ctx {
   int win_k = 0;
   Window win{};
   // persistent pivot chain of a window (spx_chain.hpp): record buffers and mode
-  unsigned long long* gr_enter = nullptr;  // CHAIN_REC granules (spx_chain.hpp layout)
-  unsigned long long* gr_ratio = nullptr;  // CHAIN_REC granules
+  unsigned long long* gr_enter = nullptr;  // ENTER_REC x CHAIN_MAX_BLOCKS granules
+  unsigned long long* gr_ratio = nullptr;  // RATIO_REC x CHAIN_MAX_BLOCKS granules
   int chain_mode = 0;      // 0: persistent chain when it fits, 1: launch per phase
   int chain_min_blocks = 0;
 

@@ -435,8 +435,12 @@ __global__ __launch_bounds__(CB) void chain_kernel(
   const int64_t j = (int64_t)b * cpb + t;
   const bool jlive = t < cpb && j < N;
   const int64_t jc = jlive ? j : 0;
-  const int64_t i = (int64_t)b * rpb + t;
-  const bool ilive = t < rpb && i < m;
+  // rows sit on waves 1.. when they fit (roff = 64), so the polling wave 0
+  // issues no row-side stores (f_q) that its next poll's vmcnt wait would
+  // also have to drain; the pivot bookkeeping is stored by the last thread
+  const int roff = rpb <= CB - 64 ? 64 : 0;
+  const int64_t i = (int64_t)b * rpb + (t - roff);
+  const bool ilive = t >= roff && t - roff < rpb && i < m;
   const int64_t ic = ilive ? i : 0;
   double o = obj[jc];
   uint32_t tg = jlive ? win.tag[jc] : 0u;
@@ -621,7 +625,8 @@ __global__ __launch_bounds__(CB) void chain_kernel(
       publish_record<NW, true>(gr_ratio, b, rec_tag(W, q, GK_RATIO), q + 1, sk,
                                [&](int ww, int64_t row, int x) -> double {
                                  if constexpr (LH)
-                                   return x == 33 ? hl33[ww] : fsl[x][(int)(row - (int64_t)b * rpb)];
+                                   return x == 33 ? hl33[ww]
+                                                  : fsl[x][(int)(row - (int64_t)b * rpb) + roff];
                                  else
                                    return hl[ww][x];
                                });
@@ -801,7 +806,7 @@ __global__ __launch_bounds__(CB) void chain_kernel(
     // p_q for the register-ring flush variants (wp; the LDS-DMA flush and
     // row_fix read the records), the pivot's bookkeeping
     if (wp && jlive) win.P[j * KW + q] = pq;
-    if (leader) {
+    if (b == 0 && t == CB - 1) {  // block 0's last thread: not in the polling wave
       st->r = r;
       st->c = c;
       st->zc = zc;

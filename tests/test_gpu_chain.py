@@ -205,3 +205,44 @@ def test_chain_timing_events(eng_cls, mode):
         out, h = e.tableau(), e.history().tolist()
     ref = _run(eng_cls, T, basis, 8, mode, max_iters=48)
     assert h == ref[1] and out.tobytes() == ref[2].tobytes()
+
+
+@pytest.mark.parametrize("K", [8, 24])
+def test_chain_basic_columns_not_unit_vectors_at_load(eng_cls, K):
+    """Basic columns that are not exact unit vectors at load (a tiny entry, a
+    -0.0, 1 + ulp) are ordinary data: the chain must not assume their values."""
+    T, basis = _random_tableau(400, 1300, seed=40 + K)
+    m = T.shape[0] - 1
+    T[3, basis[7]] = 1e-300          # basic column of row 7 with an extra entry
+    T[11, basis[2]] = -0.0           # -0.0 is not +0.0
+    T[5, basis[5]] = 1.0 + 2.0 ** -52  # not exactly 1
+    res, h, out, b, _ = _run(eng_cls, T, basis, K, 0, max_iters=3 * K + 3)
+    res1, h1, out1, b1, _ = _run(eng_cls, T, basis, K, 1, max_iters=3 * K + 3)
+    assert h == h1 and out.tobytes() == out1.tobytes() and np.array_equal(b, b1)
+    ref, rb = T.copy(), basis.copy()
+    st, hist = O.solve_tableau(ref, rb, max_iters=3 * K + 3)
+    assert [tuple(x) for x in h] == hist and np.array_equal(out, ref)
+    del m
+
+
+def test_chain_after_single_pivots_on_the_same_context(eng_cls):
+    """Single-pivot stretches and windows of different sizes on one context
+    give the single-pivot engine's sequence and bytes."""
+    T, basis = _random_tableau(300, 900, seed=77)
+    with eng_cls(0) as e:
+        e.set_window(0)
+        e.load(T, basis)
+        e.solve(max_iters=9)
+        e.set_window(16)
+        e.solve(max_iters=40)
+        e.set_window(0)
+        e.solve(max_iters=5)
+        e.set_window(24)
+        e.solve(max_iters=30)
+        h, out = e.history().tolist(), e.tableau()
+    with eng_cls(0) as e:
+        e.set_window(0)
+        e.load(T, basis)
+        e.solve(max_iters=84)
+        h0, out0 = e.history().tolist(), e.tableau()
+    assert h == h0 and out.tobytes() == out0.tobytes()
