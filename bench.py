@@ -53,10 +53,9 @@ def parse():
     ap.add_argument("--ilv", type=int, default=-1, help="elim interleaved columns (-1: default)")
     ap.add_argument("--R", type=int, default=0, help="elim rows per thread (0: auto)")
     ap.add_argument("--wgs", type=int, default=0, help="elim grid target (0: auto)")
-    ap.add_argument("--fv", type=int, default=-1,
-                    help="windowed flush: variant (bits 0-2: 0 LDS-DMA ring of 12, the default; "
-                         "6/7 rings of 9/10; 1-5 register rings, power-of-two K only) + 8 x block "
-                         "map (bits 3-5: 1 chunk-major, 2 groups rotated, 4 dynamic column claims); -1 default")
+    ap.add_argument("--fmap", type=int, default=-1,
+                    help="windowed flush block map: 0 group-major (default), 1 chunk-major, "
+                         "2 groups rotated by row chunk, 3 both; -1 default")
     ap.add_argument("--graph", type=int, default=1,
                     help="1: the timed region replays one hipGraph with an event pair "
                          "captured around every elimination; 0: direct launches + events")
@@ -183,14 +182,14 @@ def main():
         eng.set_chain(args.chain, args.chain_blocks)
     eng.load_rows(Tf, obj, basis, m, row0)
     del Tf
-    if args.nt >= 0 or args.ilv >= 0 or args.R or args.wgs or args.fv >= 0:
-        fv = max(args.fv, 0)
+    if args.nt >= 0 or args.ilv >= 0 or args.R or args.wgs or args.fmap >= 0:
+        fmap = max(args.fmap, 0) & 3
         if args.ilv >= 0:
             eng.set_elim_variant(args.R, args.wgs, -1 if args.nt < 0 else args.nt,
-                                 args.ilv | (fv & 7) << 8 | (fv >> 3 & 7) << 11)
+                                 args.ilv | fmap << 11)
         else:
             eng.set_elim_variant(args.R, args.wgs, -1 if args.nt < 0 else args.nt,
-                                 flush_variant=fv & 7, flush_map=fv >> 3 & 7)
+                                 flush_map=fmap)
     opts = dict(rule=args.rule, skip_zero_cols=not args.dense, use_graph=use_graph, chunk=32)
 
     def barrier():
@@ -277,15 +276,7 @@ def main():
     if rank == 0:
         value = n_timed / elapsed
         fvar = eng.elim_variant()
-        pow2 = K > 0 and (K & (K - 1)) == 0
-        if not K:
-            kname = "spx::elim_kernel"
-        elif fvar["flush_var"] in (1, 2, 3, 4, 5) and pow2:
-            kname = "spx::flush_kernel"
-        elif fvar["flush_var"] in (0, 1, 2, 3, 4, 5) and fvar["flush_map"] & 4:
-            kname = "spx::flush_dyn_kernel"
-        else:
-            kname = "spx::flush_lds_kernel"
+        kname = "spx::flush_lds_kernel" if K else "spx::elim_kernel"
         line = {
             "metric": METRIC,
             "value": value,

@@ -168,11 +168,11 @@ int spx_elim_timing(spx_ctx* ctx, double* total_ms, int64_t* count, int64_t* tou
  * grid target (0 = auto), non-temporal flags (bit 0 loads, bit 1 stores; -1 = auto) and
  * `interleave`: bit 0 = interleaved column assignment (else contiguous column
  * ranges), bit 1 = disable software pipelining of column pairs, bit 2 = XCD-aware
- * block swizzle, bits 8-10 = window flush variant (0 = LDS-DMA ring of 12, the
- * default; 6 / 7 = rings of 9 / 10; 1-5 = register rings, power-of-two K only),
- * bits 11-13 = window flush block map (bit 11 chunk-major, bit 12 group rotated
- * by row chunk; 0 = group-major, the default; bit 13 = records claimed
- * dynamically by the LDS-DMA flush, block map ignored). */
+ * block swizzle, bits 8-10 = window flush variant (must be 0: the LDS-DMA ring
+ * of 12; the register-ring and ring-9/10 variants were removed in round 3),
+ * bits 11-12 = window flush block map (bit 11 chunk-major, bit 12 group rotated
+ * by row chunk; 0 = group-major, the default; bit 13, the removed dynamically
+ * claimed flush, must be 0).  Returns SPX_E_ARG for a removed variant. */
 int spx_set_elim_variant(spx_ctx* ctx, int R, int target_wgs, int nt_flags, int interleave);
 /* The elimination variant in use: R, row chunks, column groups, nt flags,
  * interleave, pipelining, leading dimension. */
@@ -201,6 +201,18 @@ int spx_chain_timing(spx_ctx* ctx, double* total_ms, int64_t* count, int reset);
 int spx_set_chain(spx_ctx* ctx, int mode, int min_blocks);
 /* Blocks of the persistent chain the loaded tableau uses (0: not used). */
 int spx_get_chain(spx_ctx* ctx, int* blocks);
+/* Admission of persistent chains: a persistent chain needs all
+ * of its blocks resident at once, so the process admits, per device, chains
+ * whose blocks in flight fit a budget (default: the device's CU count, or the
+ * SPX_CHAIN_BUDGET environment variable); a call that does not fit runs its
+ * windows with the launch-per-phase chain, bit-identical.  This makes the
+ * reference's concurrent /solve calls (tests/test_performance_load.py:80,190,268)
+ * slow down instead of failing.  blocks < 0 restores the default; 0 forces the
+ * launch-per-phase chain (e.g. several processes sharing one GPU). */
+int spx_set_chain_budget(int device, int blocks);
+/* A context's admission record: out[0] calls run with the persistent chain,
+ * out[1] calls refused (launch-per-phase chain), out[2] blocks held now. */
+int spx_get_chain_stats(spx_ctx* ctx, int64_t out[3]);
 /* Layout knob: extra doubles of padding per stored column (even, 0..4096);
   * applies to the next spx_load / spx_load_rows; -1 = automatic. */
 int spx_set_ld_pad(spx_ctx* ctx, int pad);

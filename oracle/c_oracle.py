@@ -24,11 +24,18 @@ def lib():
         _lib.spxo_solve.restype = ctypes.c_int
         _lib.spxo_pivot.argtypes = [dp, i64, i64, i64, i64, ctypes.c_int]
         _lib.spxo_threads.restype = ctypes.c_int
+        _lib.spxo_set_threads.argtypes = [ctypes.c_int]
+        _lib.spxo_set_threads.restype = ctypes.c_int
     return _lib
 
 
 def threads() -> int:
     return lib().spxo_threads()
+
+
+def set_threads(n: int) -> int:
+    """OpenMP threads for the following calls (n <= 0 keeps the count); returns it."""
+    return lib().spxo_set_threads(int(n))
 
 
 def solve(T: np.ndarray, basis: np.ndarray, rule="dantzig", eps_opt=1e-9, eps_piv=1e-12,

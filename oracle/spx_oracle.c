@@ -1,8 +1,9 @@
 /*
  * spx_oracle.c — C restatement of the tableau simplex spec.
- * TEST INFRASTRUCTURE ONLY: used by tests/ as a second checker and by
- * bench.py's cpu_baseline leg as the multi-core CPU baseline.  Never linked
- * into or called by the product (simplex-solver_amd/).
+ * TEST INFRASTRUCTURE ONLY: used by tests/ as a second checker, by
+ * tests/golden/make_fullsize.py to solve the full-size configs to optimality,
+ * and by bench.py's cpu_baseline leg as the multi-core CPU baseline.  Never
+ * linked into or called by the product (simplex-solver_amd/).
  *
  * Same rules as oracle/simplex_oracle.py (which restates the pivot loop of the
  * third-party simple_simplex engine driven at reference
@@ -17,6 +18,11 @@
  *           row r = p; column c = e_r.
  * Layout: row-major (m+1) x N, objective row last.  Compile with
  * -ffp-contract=off (no FMA) so the results are bit-identical.
+ *
+ * As a CPU baseline this is the honest best of the same restatement: columns
+ * with p[j] == 0 are neither read nor written under skip_zero (the GPU skips
+ * them too), the touched columns are walked as contiguous runs so the inner
+ * loop vectorises, and rows are split over every OpenMP thread.
  */
 #include <math.h>
 #include <stdint.h>
@@ -30,6 +36,17 @@ int spxo_threads(void) {
 #ifdef _OPENMP
   return omp_get_max_threads();
 #else
+  return 1;
+#endif
+}
+
+/* Thread count for the following calls (n <= 0: leave it). Returns the count in use. */
+int spxo_set_threads(int n) {
+#ifdef _OPENMP
+  if (n > 0) omp_set_num_threads(n);
+  return omp_get_max_threads();
+#else
+  (void)n;
   return 1;
 #endif
 }
@@ -68,25 +85,39 @@ int64_t spxo_leave(const double* T, int64_t rows, int64_t cols, int64_t c, const
 void spxo_pivot(double* T, int64_t rows, int64_t cols, int64_t r, int64_t c, int skip_zero) {
   double* p = (double*)malloc(sizeof(double) * cols);
   double* f = (double*)malloc(sizeof(double) * rows);
+  int64_t* run = (int64_t*)malloc(sizeof(int64_t) * (cols + 1));  /* [begin, end) pairs */
   const double piv = T[r * cols + c];
   for (int64_t j = 0; j < cols; ++j) p[j] = T[r * cols + j] / piv;
   for (int64_t i = 0; i < rows; ++i) f[i] = T[i * cols + c];
+  /* the touched columns (p[j] != 0 under skip_zero) as contiguous runs */
+  int64_t nrun = 0;
+  for (int64_t j = 0; j < cols;) {
+    if (skip_zero && p[j] == 0.0) {
+      ++j;
+      continue;
+    }
+    const int64_t j0 = j;
+    while (j < cols && (!skip_zero || p[j] != 0.0)) ++j;
+    run[nrun++] = j0;
+    run[nrun++] = j;
+  }
 #pragma omp parallel for schedule(static)
   for (int64_t i = 0; i < rows; ++i) {
     double* row = T + i * cols;
     if (i == r) {
-      for (int64_t j = 0; j < cols; ++j)
-        if (!skip_zero || p[j] != 0.0) row[j] = p[j];
+      for (int64_t k = 0; k < nrun; k += 2)
+        for (int64_t j = run[k]; j < run[k + 1]; ++j) row[j] = p[j];
     } else {
       const double fi = f[i];
-      for (int64_t j = 0; j < cols; ++j) {
-        const double prod = fi * p[j];
-        const double upd = row[j] - prod;
-        row[j] = (!skip_zero || p[j] != 0.0) ? upd : row[j];
+      for (int64_t k = 0; k < nrun; k += 2) {
+        double* __restrict__ x = row;
+        const double* __restrict__ pp = p;
+        for (int64_t j = run[k]; j < run[k + 1]; ++j) x[j] = x[j] - fi * pp[j];
       }
     }
     row[c] = (i == r) ? 1.0 : 0.0;
   }
+  free(run);
   free(p);
   free(f);
 }

@@ -105,6 +105,8 @@ struct spx_ctx {
   State* st = nullptr;
   State* h_st = nullptr;   // pinned mirror
   State* h_poll = nullptr; // pinned [2]: State copies polled one chunk behind (spx_solve)
+  int32_t* h_stop = nullptr;  // pinned, device-visible: rank 0's time-limit stop request
+  int32_t* d_stop = nullptr;  // (sharded contexts; spx_kernels.hpp stop_requested)
   hipEvent_t ev_poll[2] = {nullptr, nullptr};
   int64_t hist_cap = 0;
 
@@ -118,7 +120,6 @@ struct spx_ctx {
   // resident flush blocks per CU, by kernel instance (every template instance has
   // its own register / LDS budget, e.g. the guarded partial-window flush)
   std::map<const void*, int> flush_bpc;
-  int flush_var = 0;       // flush kernel variant (rows per thread x columns per step)
   int flush_map = 0;       // flush block -> (row chunk, column group) map
   int flush_tail = FLUSH_TAIL_DEFAULT;  // % of the records rows moved to the tail (spx_delayed.hpp)
   int last_flush_G = 0;    // column groups of the last flush launch
@@ -136,6 +137,14 @@ struct spx_ctx {
   unsigned long long* gr_ratio = nullptr;  // RATIO_REC x CHAIN_MAX_BLOCKS granules
   int chain_mode = 0;      // 0: persistent chain when it fits, 1: launch per phase
   int chain_min_blocks = 0;
+  // admission of the persistent chain (process-wide block budget per device):
+  // blocks this context holds, calls holding them (released by a stream host
+  // callback once the call's launches have run), and whether the current call
+  // was refused (its windows then run the launch-per-phase chain)
+  int adm_blocks = 0;
+  int adm_calls = 0;
+  bool chain_denied = false;
+  int64_t chain_calls[2] = {0, 0};  // calls run with the persistent / the lazy chain
 
   // graph cache
   hipGraphExec_t gexec = nullptr;
@@ -214,7 +223,6 @@ int free_buffers(spx_ctx* ctx) {
   dfree(ctx->win.epoch);
   dfree(ctx->win.nlist);
   dfree(ctx->win.rec);
-  dfree(ctx->win.claim);
   dfree(ctx->gr_enter);
   dfree(ctx->gr_ratio);
   ctx->loaded = false;
@@ -390,8 +398,9 @@ int lazy_ratio_grid(const spx_ctx* ctx) {
 // mode, or a tableau wider than CB x CUs columns).  mode 2 / 3 force 256- /
 // 512-thread blocks; automatic: 256 threads (measured faster than 512 at
 // config 3, profiles/r02), 512 when the tableau needs more than 256 blocks.
-int chain_blocks(spx_ctx* ctx, int* cb_out = nullptr) {
+int chain_blocks(spx_ctx* ctx, int* cb_out = nullptr, bool ignore_admission = false) {
   if (ctx->sharded || ctx->chain_mode == 1) return 0;
+  if (ctx->chain_denied && !ignore_admission) return 0;
   if (!ctx->n_cu) {
     (void)hipDeviceGetAttribute(&ctx->n_cu, hipDeviceAttributeMultiprocessorCount, ctx->device);
     if (ctx->n_cu <= 0) ctx->n_cu = 256;
@@ -407,6 +416,85 @@ int chain_blocks(spx_ctx* ctx, int* cb_out = nullptr) {
   const int64_t cap = std::min<int64_t>((int64_t)ctx->n_cu, CHAIN_MAX_BLOCKS);
   return need <= cap ? (int)need : 0;
 }
+
+// ---- admission of persistent chains ("Admission") ----------
+// A persistent chain needs all of its B blocks resident at once (one per CU:
+// its LDS pin), and the chains of every context on a device share the CUs.
+// The process counts, per device, the blocks of the chains it has in flight; a
+// call whose chain would push that sum over the budget (default: the device's
+// CU count; SPX_CHAIN_BUDGET or spx_set_chain_budget override it) runs its
+// windows with the launch-per-phase chain instead, which is bit-identical and
+// needs no co-residency.  So concurrent /solve calls slow down instead of
+// timing out.  Other processes on the same GPU are not seen: give each its
+// share with SPX_CHAIN_BUDGET (0 forces the launch-per-phase chain).
+struct ChainAdmission {
+  std::mutex mu;
+  std::map<int, int> used;    // chain blocks in flight, by device
+  std::map<int, int> budget;  // explicit budgets (spx_set_chain_budget)
+};
+ChainAdmission& adm() {
+  static ChainAdmission a;
+  return a;
+}
+
+int adm_budget_locked(ChainAdmission& a, const spx_ctx* ctx) {
+  const auto it = a.budget.find(ctx->device);
+  if (it != a.budget.end()) return it->second;
+  if (const char* e = std::getenv("SPX_CHAIN_BUDGET")) return std::max(0, std::atoi(e));
+  return ctx->n_cu;
+}
+
+// Decide the chain of the call starting now.  Returns true when the call holds
+// a reservation, which adm_release must return once the call's launches ran.
+bool adm_acquire(spx_ctx* ctx) {
+  const bool was = ctx->chain_denied;
+  ctx->chain_denied = false;
+  const int B = ctx->win_k ? chain_blocks(ctx, nullptr, true) : 0;
+  if (B <= 0) return false;  // no persistent chain for this call anyway
+  ChainAdmission& a = adm();
+  bool ok;
+  {
+    std::lock_guard<std::mutex> lk(a.mu);
+    const int cap = adm_budget_locked(a, ctx);
+    int& used = a.used[ctx->device];
+    const int extra = std::max(0, B - ctx->adm_blocks);  // 0: this context holds B already
+    ok = used + extra <= cap;
+    if (ok) {
+      used += extra;
+      ctx->adm_blocks += extra;
+      ctx->adm_calls++;
+    }
+  }
+  ctx->chain_denied = !ok;
+  ctx->chain_calls[ok ? 0 : 1]++;
+  if (ctx->chain_denied != was) drop_graphs(ctx);  // the cached graph has the other chain
+  return ok;
+}
+
+void adm_release(spx_ctx* ctx) {
+  ChainAdmission& a = adm();
+  std::lock_guard<std::mutex> lk(a.mu);
+  if (ctx->adm_calls > 0 && --ctx->adm_calls == 0) {
+    a.used[ctx->device] -= ctx->adm_blocks;
+    ctx->adm_blocks = 0;
+  }
+}
+
+void adm_release_cb(void* p) { adm_release(static_cast<spx_ctx*>(p)); }
+
+// Holds a call's reservation: released at once when the call drained its
+// stream, else by a host callback behind the call's launches on the stream.
+struct AdmCall {
+  spx_ctx* ctx;
+  bool held = false;
+  bool drained = false;
+  explicit AdmCall(spx_ctx* c) : ctx(c) {}
+  ~AdmCall() {
+    if (!held) return;
+    if (drained || hipLaunchHostFunc(ctx->stream, adm_release_cb, ctx) != hipSuccess)
+      adm_release(ctx);
+  }
+};
 
 // An event pair from the context's pool (created on first use).
 int next_event_pair(spx_ctx* ctx, std::vector<std::pair<hipEvent_t, hipEvent_t>>& pool,
@@ -426,10 +514,6 @@ int enqueue_window_t(spx_ctx* ctx, int npiv, bool time_flush) {
   const int nbw = lazy_ratio_grid(ctx);
   int cb = BLK;
   const int B = chain_blocks(ctx, &cb);
-  // the register-ring flush variants read p_s[j] from P; the LDS-DMA flush
-  // and row_fix read the window's records
-  constexpr bool POW2K = (KMAX & (KMAX - 1)) == 0;
-  const bool reg_ring_flush = POW2K && ctx->flush_var >= 1 && ctx->flush_var <= 5;
   std::pair<hipEvent_t, hipEvent_t>* ec = nullptr;
   if (ctx->time_chain) {
     int rc = next_event_pair(ctx, ctx->evc, ctx->evc_used, &ec);
@@ -443,8 +527,7 @@ int enqueue_window_t(spx_ctx* ctx, int npiv, bool time_flush) {
     hipLaunchKernelGGL(kern, dim3(B), dim3(cb), 0, ctx->stream, ctx->enter_part, ctx->st,
                        (const Params*)ctx->prm, std::max(NWAVE * ctx->nbn, B),
                        (const double*)ctx->A, ctx->ld, ctx->m_local, ctx->N, ctx->obj, ctx->win,
-                       npiv, ctx->basis, ctx->hist, ctx->gr_enter, ctx->gr_ratio, cpb, rpb,
-                       reg_ring_flush ? 1 : 0);
+                       npiv, ctx->basis, ctx->hist, ctx->gr_enter, ctx->gr_ratio, cpb, rpb);
   }
   for (int q = 0; B == 0 && q < npiv; ++q) {
     hipLaunchKernelGGL(lazy_ratio_kernel<KMAX>, dim3(nbw), dim3(BLK), 0, ctx->stream,
@@ -465,7 +548,7 @@ int enqueue_window_t(spx_ctx* ctx, int npiv, bool time_flush) {
                          (const Key*)ctx->ratio_part, (const State*)ctx->st,
                          (const Params*)ctx->prm, NWAVE * nbw, q, (const double*)ctx->A,
                          ctx->ld, ctx->m_local, ctx->row0, ctx->N, ctx->win, ctx->sendbuf,
-                         ctx->rank);
+                         ctx->rank, (const int32_t*)ctx->d_stop);
       const int rc = comm_allgather(ctx);
       if (rc) return rc;
       hipLaunchKernelGGL((lazy_norm_kernel<KMAX, true>), dim3(ctx->nbn), dim3(BLK), 0,
@@ -496,35 +579,13 @@ int enqueue_window_t(spx_ctx* ctx, int npiv, bool time_flush) {
                        ctx->st, ctx->flush_map | ctx->flush_tail << 8);
   };
   const bool nts = (ctx->elim_nt & 2) != 0;
-  // variants: 0 (default) LDS-DMA ring of 12 columns per wave over the
-  // compacted records; 6 / 7 the same with rings of 9 / 10; register rings
-  // (rows per lane x depth, A = sweep direction alternating per window):
-  // 1 2x4, 2 4x4, 3 4x4A, 4 2x8, 5 2x4A (profiles/r01/tune_flush_*.log)
-  // (register rings exist for power-of-two windows only; others take the default)
-  constexpr bool POW2 = (KMAX & (KMAX - 1)) == 0;
-  switch (POW2 || ctx->flush_var >= 6 ? ctx->flush_var : 0) {
-    case 1: if constexpr (POW2) { nts ? go(flush_kernel<KMAX, 2, 4, true>, 2) : go(flush_kernel<KMAX, 2, 4, false>, 2); } break;
-    case 2: if constexpr (POW2) { nts ? go(flush_kernel<KMAX, 4, 4, true>, 4) : go(flush_kernel<KMAX, 4, 4, false>, 4); } break;
-    case 3: if constexpr (POW2) { nts ? go(flush_kernel<KMAX, 4, 4, true, true>, 4) : go(flush_kernel<KMAX, 4, 4, false, true>, 4); } break;
-    case 4: if constexpr (POW2) { nts ? go(flush_kernel<KMAX, 2, 8, true>, 2) : go(flush_kernel<KMAX, 2, 8, false>, 2); } break;
-    case 5: if constexpr (POW2) { nts ? go(flush_kernel<KMAX, 2, 4, true, true>, 2) : go(flush_kernel<KMAX, 2, 4, false, true>, 2); } break;
-    case 6: nts ? go(flush_lds_kernel<KMAX, 9, true>, 2) : go(flush_lds_kernel<KMAX, 9, false>, 2); break;
-    case 7: nts ? go(flush_lds_kernel<KMAX, 10, true>, 2) : go(flush_lds_kernel<KMAX, 10, false>, 2); break;
-    default:
-      if (ctx->flush_map & 4) {  // records claimed dynamically (a claimer wave per block)
-        if (npiv < KMAX)
-          nts ? go(flush_dyn_kernel<KMAX, 12, true, true>, 2, BLK + 64)
-              : go(flush_dyn_kernel<KMAX, 12, false, true>, 2, BLK + 64);
-        else
-          nts ? go(flush_dyn_kernel<KMAX, 12, true>, 2, BLK + 64)
-              : go(flush_dyn_kernel<KMAX, 12, false>, 2, BLK + 64);
-        break;
-      }
-      if (npiv < KMAX)  // the last window of a request: every slot guarded
-        nts ? go(flush_lds_kernel<KMAX, 12, true, true>, 2) : go(flush_lds_kernel<KMAX, 12, false, true>, 2);
-      else
-        nts ? go(flush_lds_kernel<KMAX, 12, true>, 2) : go(flush_lds_kernel<KMAX, 12, false>, 2);
-  }
+  // the LDS-DMA ring of 12 columns per wave over the window's compacted
+  // records (the register-ring and dynamically claimed flushes
+  // measured slower in rounds 1-2 and were removed)
+  if (npiv < KMAX)  // the last window of a request: every slot guarded
+    nts ? go(flush_lds_kernel<KMAX, 12, true, true>, 2) : go(flush_lds_kernel<KMAX, 12, false, true>, 2);
+  else
+    nts ? go(flush_lds_kernel<KMAX, 12, true>, 2) : go(flush_lds_kernel<KMAX, 12, false>, 2);
   if (e) {
     const int rc = record_event(ctx, e->second);
     if (rc) return rc;
@@ -556,7 +617,7 @@ int enqueue_pivot(spx_ctx* ctx, bool time_elim) {
   } else {
     hipLaunchKernelGGL(prep_kernel, dim3(ctx->nbn), dim3(BLK), 0, ctx->stream, ctx->A, ctx->ld,
                        ctx->m_local, ctx->row0, ctx->N, ctx->F, ctx->ratio_part, ctx->sendbuf,
-                       ctx->rank, ctx->st);
+                       ctx->rank, ctx->st, (const int32_t*)ctx->d_stop);
     int rc = comm_allgather(ctx);
     if (rc) return rc;
     launch_norm<MODE_FINISH>(ctx);
@@ -626,7 +687,8 @@ int pull_state(spx_ctx* ctx) {
 
 // Prepare a pivot call: params, status RUNNING, fresh entering partials and
 // the primed first pivot (rule-chosen, or the forced (fr, fc) of spx_pivot_at).
-int begin_call(spx_ctx* ctx, const spx_opts* o, int64_t fc = -1, int64_t fr = -1) {
+int begin_call(spx_ctx* ctx, const spx_opts* o, AdmCall* adm_call, int64_t fc = -1,
+               int64_t fr = -1) {
   if (!ctx->loaded) {
     ctx->err = "no tableau loaded";
     return SPX_E_STATE;
@@ -635,6 +697,7 @@ int begin_call(spx_ctx* ctx, const spx_opts* o, int64_t fc = -1, int64_t fr = -1
   (void)hipGetLastError();  // drop a stale error of an unrelated earlier call
   int rc = pull_state(ctx);
   if (rc) return rc;
+  if (ctx->h_stop) __atomic_store_n(ctx->h_stop, 0, __ATOMIC_SEQ_CST);  // (stream drained above)
   if ((rc = write_params(ctx, o))) return rc;
   if ((rc = set_state_fields(ctx, ST_RUNNING, fc, fr))) return rc;
   launch_norm<MODE_INIT>(ctx);
@@ -646,6 +709,7 @@ int begin_call(spx_ctx* ctx, const spx_opts* o, int64_t fc = -1, int64_t fr = -1
                        ctx->enter_part + ctx->nbn, n);
   }
   HIPC(hipGetLastError());
+  adm_call->held = adm_acquire(ctx);  // persistent or launch-per-phase chain for this call
   return SPX_OK;
 }
 
@@ -682,18 +746,15 @@ int map_status(int32_t st) {
     case ST_UNBOUNDED: return SPX_UNBOUNDED;
     case ST_LIMIT: return SPX_ITER_LIMIT;
     case ST_FAULT: return SPX_E_STATE;
-    case ST_FLUSH_FAULT: return SPX_E_STATE;
     default: return SPX_RUNNING;
   }
 }
 
-bool is_fault(int32_t st) { return st == ST_FAULT || st == ST_FLUSH_FAULT; }
+bool is_fault(int32_t st) { return st == ST_FAULT; }
 
 // The device reported a fault (an in-launch exchange timed out).
 int fault(spx_ctx* ctx) {
-  ctx->err = ctx->h_st->status == ST_FLUSH_FAULT
-                 ? "device fault: a flush batch hand-off timed out"
-                 : "device fault: a pivot-chain exchange timed out (blocks not co-resident?)";
+  ctx->err = "device fault: a pivot-chain exchange timed out (blocks not co-resident?)";
   return SPX_E_STATE;
 }
 
@@ -736,9 +797,6 @@ int alloc_common(spx_ctx* ctx, int64_t m_local, int64_t N, int64_t m_global, int
     HIPC(hipMemsetAsync(ctx->win.c, 0, sizeof(int64_t) * KW, ctx->stream));
     HIPC(hipMemsetAsync(ctx->win.tag, 0, sizeof(uint32_t) * N, ctx->stream));
     HIPC(hipMemsetAsync(ctx->win.epoch, 0, sizeof(uint32_t), ctx->stream));
-    ctx->win.nclaim = (int)std::max<int64_t>(1, (m_local + 2 * BLK - 1) / (2 * BLK));
-    HIPC(hipMalloc(&ctx->win.claim, sizeof(uint32_t) * ctx->win.nclaim));
-    HIPC(hipMemsetAsync(ctx->win.claim, 0, sizeof(uint32_t) * ctx->win.nclaim, ctx->stream));
     const size_t ge = sizeof(unsigned long long) * ENTER_REC * CHAIN_MAX_BLOCKS;
     const size_t gq = sizeof(unsigned long long) * RATIO_REC * CHAIN_MAX_BLOCKS;
     HIPC(hipMalloc(&ctx->gr_enter, ge));
@@ -797,6 +855,8 @@ int spx_create(spx_ctx** out, int device) {
   if (e == hipSuccess) e = hipMalloc(&ctx->st, sizeof(State));
   if (e == hipSuccess) e = hipHostMalloc(&ctx->h_st, sizeof(State), hipHostMallocDefault);
   if (e == hipSuccess) e = hipHostMalloc(&ctx->h_poll, 2 * sizeof(State), hipHostMallocDefault);
+  if (e == hipSuccess) e = hipHostMalloc(&ctx->h_stop, sizeof(int32_t), hipHostMallocMapped);
+  if (e == hipSuccess) e = hipHostGetDevicePointer((void**)&ctx->d_stop, ctx->h_stop, 0);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->ev_poll[0], hipEventDisableTiming);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->ev_poll[1], hipEventDisableTiming);
   if (e != hipSuccess) {
@@ -805,6 +865,7 @@ int spx_create(spx_ctx** out, int device) {
     return SPX_E_HIP;
   }
   std::memset(ctx->h_st, 0, sizeof(State));
+  *ctx->h_stop = 0;
   // tuning hook: SPX_FLUSH_TAIL=x (0..50) overrides the flush's tail share
   if (const char* ft = std::getenv("SPX_FLUSH_TAIL"))
     ctx->flush_tail = std::max(0, std::min(50, std::atoi(ft)));
@@ -885,6 +946,7 @@ int spx_destroy(spx_ctx* ctx) {
   if (ctx->ev_done) (void)hipEventDestroy(ctx->ev_done);
   (void)hipSetDevice(ctx->device);
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+  while (ctx->adm_calls > 0) adm_release(ctx);  // (callbacks ran at the sync; error paths)
   free_buffers(ctx);
   for (auto* pool : {&ctx->ev, &ctx->evc})
     for (auto& e : *pool) {
@@ -896,6 +958,7 @@ int spx_destroy(spx_ctx* ctx) {
   dfree(ctx->st);
   if (ctx->h_st) (void)hipHostFree(ctx->h_st);
   if (ctx->h_poll) (void)hipHostFree(ctx->h_poll);
+  if (ctx->h_stop) (void)hipHostFree(ctx->h_stop);
   for (hipEvent_t ev : ctx->ev_poll)
     if (ev) (void)hipEventDestroy(ev);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
@@ -1052,7 +1115,8 @@ int spx_solve(spx_ctx* ctx, const spx_opts* opts, spx_result* res) {
   spx_default_opts(&d);
   const spx_opts* o = opts ? opts : &d;
   const auto t0 = std::chrono::steady_clock::now();
-  int rc = begin_call(ctx, o);
+  AdmCall adm_call(ctx);
+  int rc = begin_call(ctx, o, &adm_call);
   if (rc) return rc;
   const int64_t it0 = ctx->h_st->iters;
   const int chunk = ctx->win_k ? ctx->win_k : (o->chunk > 0 ? o->chunk : 32);
@@ -1086,12 +1150,19 @@ int spx_solve(spx_ctx* ctx, const spx_opts* opts, spx_result* res) {
     if (status != SPX_RUNNING) break;
     const double el =
         std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-    if (o->time_limit_s > 0 && el >= o->time_limit_s && !ctx->sharded) {
-      status = SPX_ITER_LIMIT;
-      break;
+    if (o->time_limit_s > 0 && el >= o->time_limit_s) {
+      if (!ctx->sharded) {
+        status = SPX_ITER_LIMIT;
+        break;
+      }
+      // a row shard stops where every rank stops: rank 0 asks its device,
+      // whose payload carries the request to all ranks before the same pivot
+      // (status ST_LIMIT, read at a later poll); the other ranks wait for it
+      if (ctx->rank == 0 && ctx->h_stop) __atomic_store_n(ctx->h_stop, 1, __ATOMIC_SEQ_CST);
     }
   }
   if ((rc = pull_state(ctx))) return rc;  // the final state (after the extra chunk)
+  adm_call.drained = true;
   if (status < 0 || is_fault(ctx->h_st->status)) return fault(ctx);
   double z = 0.0;
   HIPC(hipMemcpyAsync(&z, ctx->obj + (ctx->N - 1), sizeof(double), hipMemcpyDeviceToHost,
@@ -1110,11 +1181,13 @@ int spx_solve(spx_ctx* ctx, const spx_opts* opts, spx_result* res) {
 
 int spx_pivot(spx_ctx* ctx, const spx_opts* opts, int64_t* r, int64_t* c) {
   if (!ctx) return SPX_E_ARG;
-  int rc = begin_call(ctx, opts);
+  AdmCall adm_call(ctx);
+  int rc = begin_call(ctx, opts, &adm_call);
   if (rc) return rc;
   const int64_t it0 = ctx->h_st->iters;
   if ((rc = enqueue_pivots(ctx, 1, 0))) return rc;
   if ((rc = pull_state(ctx))) return rc;
+  adm_call.drained = true;
   const int status = map_status(ctx->h_st->status);
   if (status < 0) return fault(ctx);
   if (status == SPX_RUNNING && ctx->h_st->iters == it0 + 1) {
@@ -1131,11 +1204,13 @@ int spx_pivot_at(spx_ctx* ctx, int64_t r, int64_t c) {
   if (!ctx) return SPX_E_ARG;
   CHECK_ARG(ctx->loaded && r >= 0 && r < ctx->m_global && c >= 0 && c < ctx->N - 1,
             "pivot position out of range");
-  int rc = begin_call(ctx, nullptr, c, r);
+  AdmCall adm_call(ctx);
+  int rc = begin_call(ctx, nullptr, &adm_call, c, r);
   if (rc) return rc;
   if ((rc = enqueue_pivots(ctx, 1, 0))) return rc;
   // pull the post-pivot state before writing the forced fields back
   if ((rc = pull_state(ctx))) return rc;
+  adm_call.drained = true;
   const int32_t st_after = ctx->h_st->status;
   if (is_fault(st_after)) return fault(ctx);
   if ((rc = set_state_fields(ctx, st_after, -1, -1))) return rc;
@@ -1149,7 +1224,8 @@ int spx_run_pivots(spx_ctx* ctx, const spx_opts* opts, int64_t npivots, int time
   spx_opts d;
   spx_default_opts(&d);
   const spx_opts* o = opts ? opts : &d;
-  int rc = begin_call(ctx, o);
+  AdmCall adm_call(ctx);  // released behind this call's launches (it does not sync)
+  int rc = begin_call(ctx, o, &adm_call);
   if (rc) return rc;
   // (chain timing records one event pair per window: direct launches, since a
   // replayed graph re-records the same captured events)
@@ -1311,14 +1387,17 @@ int spx_elim_timing(spx_ctx* ctx, double* total_ms, int64_t* count, int64_t* tou
 // column assignment.
 int spx_set_elim_variant(spx_ctx* ctx, int R, int target_wgs, int nt_flags, int interleave) {
   if (!ctx) return SPX_E_ARG;
+  // bits 8-10 (flush variant) and 13 (dynamic claims) selected flush kernels
+  // that measured slower and were removed: only 0 remains
+  CHECK_ARG(((interleave >> 8) & 7) == 0 && ((interleave >> 13) & 1) == 0,
+            "flush variant must be 0 (the LDS-DMA ring); block map bits 11-12 only");
   ctx->tune_R = R;
   ctx->tune_wgs = target_wgs;
   ctx->tune_nt = nt_flags < 0 ? -1 : (nt_flags & 3);
   ctx->elim_ilv = interleave & 1;
   ctx->elim_pipe = (interleave & 2) ? 0 : 1;  // bit 1 of `interleave`: disable pipelining
   ctx->elim_xcd = (interleave & 4) ? 1 : 0;   // bit 2: XCD-aware block swizzle
-  ctx->flush_var = (interleave >> 8) & 7;     // bits 8-10: windowed flush variant
-  ctx->flush_map = (interleave >> 11) & 7;    // bits 11-13: flush block map (4: dynamic claims)
+  ctx->flush_map = (interleave >> 11) & 3;    // bits 11-12: flush block map
   choose_geometry(ctx);  // also resolves the automatic nt flags
   if (ctx->loaded) {
     if (ctx->rch > ctx->nbr) {  // ratio_part must hold rch partials
@@ -1394,7 +1473,30 @@ int spx_set_chain(spx_ctx* ctx, int mode, int min_blocks) {
 // Blocks of the persistent chain for the loaded tableau (0: not used).
 int spx_get_chain(spx_ctx* ctx, int* blocks) {
   if (!ctx || !blocks) return SPX_E_ARG;
-  *blocks = ctx->loaded && ctx->win_k ? chain_blocks(ctx) : 0;
+  *blocks = ctx->loaded && ctx->win_k ? chain_blocks(ctx, nullptr, true) : 0;
+  return SPX_OK;
+}
+
+// Process-wide budget of persistent-chain blocks in flight on `device`
+// (admission); blocks < 0 restores the default (SPX_CHAIN_BUDGET,
+// else the device's CU count).
+int spx_set_chain_budget(int device, int blocks) {
+  ChainAdmission& a = adm();
+  std::lock_guard<std::mutex> lk(a.mu);
+  if (blocks < 0) a.budget.erase(device);
+  else a.budget[device] = blocks;
+  return SPX_OK;
+}
+
+// Admission record of a context: calls run with the persistent chain, calls
+// refused (launch-per-phase chain instead), blocks it holds right now.
+int spx_get_chain_stats(spx_ctx* ctx, int64_t out[3]) {
+  if (!ctx || !out) return SPX_E_ARG;
+  ChainAdmission& a = adm();
+  std::lock_guard<std::mutex> lk(a.mu);
+  out[0] = ctx->chain_calls[0];
+  out[1] = ctx->chain_calls[1];
+  out[2] = ctx->adm_blocks;
   return SPX_OK;
 }
 
@@ -1403,7 +1505,7 @@ int spx_get_chain(spx_ctx* ctx, int* blocks) {
 // the last flush launch (0 before the first).
 int spx_get_flush_variant(const spx_ctx* ctx, int64_t out[4]) {
   if (!ctx || !out) return SPX_E_ARG;
-  out[0] = ctx->flush_var;
+  out[0] = 0;  // the LDS-DMA ring (the only flush since round 3)
   out[1] = ctx->flush_map;
   out[2] = ctx->last_flush_rch;
   out[3] = ctx->last_flush_G;

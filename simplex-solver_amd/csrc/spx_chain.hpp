@@ -72,17 +72,41 @@ constexpr int RATIO_HDR = 4;            // v_lo, v_hi, row, t (t read under Blan
 constexpr int RATIO_REC = RATIO_HDR + 2 + 2 * 32;  // + RHS of row (lo, hi), f_0..f_q[row]
 constexpr int CHAIN_MAX_BLOCKS = 256;   // one block per CU
 constexpr unsigned CHAIN_SPIN_MAX = 1u << 22;
+// Row-sharded chain (chain_kernel<.., SH = true>): the ratio
+// records of every rank's blocks land in every rank's buffer, at block slot
+// rank * B + b of planes CHAIN_SH_SLOTS apart; two halves by pivot parity, then
+// one plane of window-end granules.
+constexpr int CHAIN_MAX_RANKS = 16;
+constexpr int CHAIN_SH_SLOTS = 512;     // nranks x B ratio records (8 per polling lane)
+constexpr int CHAIN_SH_PLANES = 2 * RATIO_REC + 1;
 
 typedef __attribute__((address_space(1))) unsigned long long gu64;
 typedef __attribute__((address_space(1))) unsigned gu32;
 
+// Granule store / load: agent scope on one GPU; system scope (SYS) for the
+// sharded chain's records, which peers on other GPUs write over xGMI
+template <bool SYS = false>
 __device__ __forceinline__ void g_store(gu64* g, unsigned tag, unsigned val) {
   __hip_atomic_store(g, ((unsigned long long)tag << 32) | val, __ATOMIC_RELAXED,
-                     __HIP_MEMORY_SCOPE_AGENT);
+                     SYS ? __HIP_MEMORY_SCOPE_SYSTEM : __HIP_MEMORY_SCOPE_AGENT);
 }
+template <bool SYS = false>
 __device__ __forceinline__ unsigned long long g_load(const gu64* g) {
-  return __hip_atomic_load(const_cast<gu64*>(g), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return __hip_atomic_load(const_cast<gu64*>(g), __ATOMIC_RELAXED,
+                           SYS ? __HIP_MEMORY_SCOPE_SYSTEM : __HIP_MEMORY_SCOPE_AGENT);
 }
+
+// The row-sharded chain's view of the other ranks (a kernel argument): their
+// ratio-record buffers and stale tableaux (peer pointers: IPC-mapped across
+// processes, plain device pointers between the virtual ranks of one process).
+struct ChainPeers {
+  int rank, nranks;
+  unsigned long long* ratio[CHAIN_MAX_RANKS];  // CHAIN_SH_PLANES x CHAIN_SH_SLOTS granules each
+  const double* A[CHAIN_MAX_RANKS];
+  int64_t ld[CHAIN_MAX_RANKS];
+  int64_t row0[CHAIN_MAX_RANKS];
+  const int32_t* stop_req;  // rank 0: the host's time-limit stop request (pinned)
+};
 // write-through (sc1) store / load of one double
 __device__ __forceinline__ void wt_store(double* p, double v) {
   __hip_atomic_store((gu64*)p, (unsigned long long)__double_as_longlong(v), __ATOMIC_RELAXED,
@@ -98,6 +122,7 @@ __device__ __forceinline__ void drain_stores() { asm volatile("s_waitcnt vmcnt(0
 // granule kinds
 constexpr int GK_RATIO = 0;  // ratio record of slot q
 constexpr int GK_ENTER = 1;  // entering record published by slot q (for slot q+1)
+constexpr int GK_DONE = 2;   // sharded: a block's last row gather of the window returned
 // granule tag: never 0 (the buffers start zeroed), unique per (epoch, slot, kind)
 __device__ __forceinline__ unsigned rec_tag(uint32_t epoch, int q, int kind) {
   return 0x80000000u | ((epoch & 0x7fffffu) << 8) | ((unsigned)q << 2) | (unsigned)kind;
@@ -225,24 +250,27 @@ __device__ __forceinline__ bool spin_fail(unsigned& spins, State* st) {
 // G the header granules read (3, or 4 for Bland's ratio records).
 template <bool RATIO>
 __device__ __forceinline__ void decode_record(KeyP& k, const unsigned long long (&g)[4], int b,
-                                              int rule) {
+                                              int rule, unsigned& stop) {
   const double v = g_decode_d(g[0], g[1]);
   const unsigned idx = (unsigned)g[2];
+  // granule 3 of a ratio record: t (bits 0-30) and the sharded chain's stop
+  // request (bit 31; rank 0's blocks)
+  if (RATIO) stop |= (unsigned)g[3] >> 31;
   if (idx == 0xffffffffu) return;
   if constexpr (RATIO) {
     // Dantzig ties go to the lowest row (t = row); Bland's to the lowest
     // basic-variable index (granule 3)
-    kmin2(k, v, rule == RULE_BLAND ? (int64_t)(unsigned)g[3] : (int64_t)idx, (int64_t)idx, 0.0,
-          (double)b);
+    kmin2(k, v, rule == RULE_BLAND ? (int64_t)((unsigned)g[3] & 0x7fffffffu) : (int64_t)idx,
+          (int64_t)idx, 0.0, (double)b);
   } else {
     // Dantzig: most negative reduced cost; Bland: lowest index (key 0)
     kmin2(k, rule == RULE_BLAND ? 0.0 : v, (int64_t)idx, (int64_t)idx, v, (double)b);
   }
 }
 
-template <bool RATIO, int G, int RPL>
-__device__ __forceinline__ bool poll_records_n(const gu64* recs, int B, unsigned tag, int rule,
-                                               KeyP& k, State* st) {
+template <bool RATIO, int G, int RPL, bool SYS>
+__device__ __forceinline__ bool poll_records_n(const gu64* recs, int B, int rs, unsigned tag,
+                                               int rule, KeyP& k, State* st, bool* stop) {
   const int lane = threadIdx.x & 63;
   // lane l reads blocks l, l+64, ... (RPL records): every load of a pass is
   // issued before the first tag check, so a pass is one round trip (one pass
@@ -254,7 +282,7 @@ __device__ __forceinline__ bool poll_records_n(const gu64* recs, int B, unsigned
       const int b = min(lane + 64 * x, B - 1);  // clamped: no branch around the loads
 #pragma unroll
       for (int u = 0; u < 4; ++u)
-        g[x][u] = u < G ? g_load(recs + (size_t)u * CHAIN_MAX_BLOCKS + b)
+        g[x][u] = u < G ? g_load<SYS>(recs + (size_t)u * rs + b)
                         : (unsigned long long)tag << 32;
     }
     bool ok = true;
@@ -264,9 +292,11 @@ __device__ __forceinline__ bool poll_records_n(const gu64* recs, int B, unsigned
       for (int u = 0; u < 4; ++u) ok &= (unsigned)(g[x][u] >> 32) == tag;
     if (__all(ok)) {
       k = keyp_none();
+      unsigned sb = 0u;
 #pragma unroll
       for (int x = 0; x < RPL; ++x)
-        if (lane + 64 * x < B) decode_record<RATIO>(k, g[x], lane + 64 * x, rule);
+        if (lane + 64 * x < B) decode_record<RATIO>(k, g[x], lane + 64 * x, rule, sb);
+      if (stop) *stop = __ballot(sb != 0u) != 0ull;
       break;
     }
     if (spin_fail(spins, st)) return false;
@@ -280,31 +310,34 @@ __device__ __forceinline__ bool poll_records_n(const gu64* recs, int B, unsigned
   return true;
 }
 
-template <bool RATIO, int G>
-__device__ __forceinline__ bool poll_records(const gu64* recs, int B, unsigned tag, int rule,
-                                             KeyP& k, State* st) {
-  if (B <= 64) return poll_records_n<RATIO, G, 1>(recs, B, tag, rule, k, st);
-  if (B <= 128) return poll_records_n<RATIO, G, 2>(recs, B, tag, rule, k, st);
-  return poll_records_n<RATIO, G, 4>(recs, B, tag, rule, k, st);
+template <bool RATIO, int G, bool SYS = false>
+__device__ __forceinline__ bool poll_records(const gu64* recs, int B, int rs, unsigned tag,
+                                             int rule, KeyP& k, State* st,
+                                             bool* stop = nullptr) {
+  if (B <= 64) return poll_records_n<RATIO, G, 1, SYS>(recs, B, rs, tag, rule, k, st, stop);
+  if (B <= 128) return poll_records_n<RATIO, G, 2, SYS>(recs, B, rs, tag, rule, k, st, stop);
+  if (!SYS || B <= 256)
+    return poll_records_n<RATIO, G, 4, SYS>(recs, B, rs, tag, rule, k, st, stop);
+  return poll_records_n<RATIO, G, 8, SYS>(recs, B, rs, tag, rule, k, st, stop);
 }
 
 // The dependent loads of a phase from the winning record (block wb): lane
 // s < n reads the history pair at planes h0 + 2s, h0 + 2s + 1, and every lane
 // reads NE wave-uniform pairs at planes e0 + 2x.  One pass re-reads until every
 // granule carries the record's tag.  Returns false on timeout.
-template <int NE>
-__device__ __forceinline__ bool load_extras(const gu64* rec, int wb, int h0, int n, int e0,
+template <int NE, bool SYS = false>
+__device__ __forceinline__ bool load_extras(const gu64* rec, int rs, int wb, int h0, int n, int e0,
                                             unsigned tag, double& hv, double (&ev)[2],
                                             State* st) {
   const int lane = threadIdx.x & 63;
   const bool mine = lane < n;
-  const gu64* g = rec + (size_t)(h0 + 2 * (mine ? lane : 0)) * CHAIN_MAX_BLOCKS + wb;
-  const gu64* e = rec + (size_t)e0 * CHAIN_MAX_BLOCKS + wb;
+  const gu64* g = rec + (size_t)(h0 + 2 * (mine ? lane : 0)) * rs + wb;
+  const gu64* e = rec + (size_t)e0 * rs + wb;
   for (unsigned spins = 0;;) {
-    const unsigned long long lo = g_load(g), hi = g_load(g + CHAIN_MAX_BLOCKS);
+    const unsigned long long lo = g_load<SYS>(g), hi = g_load<SYS>(g + rs);
     unsigned long long x[2 * NE > 0 ? 2 * NE : 1];
 #pragma unroll
-    for (int u = 0; u < 2 * NE; ++u) x[u] = g_load(e + (size_t)u * CHAIN_MAX_BLOCKS);
+    for (int u = 0; u < 2 * NE; ++u) x[u] = g_load<SYS>(e + (size_t)u * rs);
     bool good = !mine || ((unsigned)(lo >> 32) == tag && (unsigned)(hi >> 32) == tag);
 #pragma unroll
     for (int u = 0; u < 2 * NE; ++u) good &= (unsigned)(x[u] >> 32) == tag;
@@ -324,9 +357,10 @@ __device__ __forceinline__ bool load_extras(const gu64* rec, int wb, int h0, int
 // keys (every lane the same winner), its lanes store the winner's extras, then
 // lane 0 the header (program order: the extras leave first).  RATIO: header v,
 // row, t; extras [extra, history].
-template <int NW, bool RATIO, typename Hist>
-__device__ __forceinline__ void publish_record(gu64* rec, int b, unsigned tag, int nh,
-                                               const KeyP (&sk)[NW], Hist hist) {
+template <int NW, bool RATIO, bool SYS = false, typename Dst, typename Hist>
+__device__ __forceinline__ void publish_record(Dst dst, int nd, int rs, unsigned tag, int nh,
+                                               const KeyP (&sk)[NW], Hist hist,
+                                               unsigned stopbit = 0u) {
   const int lane = threadIdx.x & 63;
   KeyP k;
   if constexpr (NW == 4) {
@@ -343,29 +377,39 @@ __device__ __forceinline__ void publish_record(gu64* rec, int b, unsigned tag, i
   }
   const int ww = (int)k.b;  // the winning wave (a payload slot of the block key)
   const bool none = k.row < 0;
-  gu64* rb = rec + b;
   constexpr int H0 = RATIO ? RATIO_HDR + 2 : ENTER_HDR;  // first history plane
+  // this lane's granule (the same for every destination): lane x < 2*nh
+  // history granule x; RATIO: lanes 62, 63 the extra (row's RHS)
+  // (lanes 62, 63 may store both: slot 31's history and the extra)
+  int plane = -1, plane2 = -1;
+  unsigned val = 0u, val2 = 0u;
   if (!none) {
-    // lane x < 2*nh: history granule x; RATIO: lanes 62, 63 the extra (row's RHS)
     if (lane < 2 * nh) {
       const unsigned long long x =
           (unsigned long long)__double_as_longlong(hist(ww, k.row, lane >> 1));
-      g_store(rb + (size_t)(H0 + lane) * CHAIN_MAX_BLOCKS, tag,
-              (lane & 1) ? (unsigned)(x >> 32) : (unsigned)x);
+      plane = H0 + lane;
+      val = (lane & 1) ? (unsigned)(x >> 32) : (unsigned)x;
     }
     if (RATIO && lane >= 62) {
       const unsigned long long x =
           (unsigned long long)__double_as_longlong(hist(ww, k.row, 33));
-      g_store(rb + (size_t)(RATIO_HDR + (lane - 62)) * CHAIN_MAX_BLOCKS, tag,
-              (lane & 1) ? (unsigned)(x >> 32) : (unsigned)x);
+      plane2 = RATIO_HDR + (lane - 62);
+      val2 = (lane & 1) ? (unsigned)(x >> 32) : (unsigned)x;
     }
   }
-  if (lane == 0) {
-    const unsigned long long vb = (unsigned long long)__double_as_longlong(RATIO ? k.v : k.a);
-    g_store(rb + 0 * CHAIN_MAX_BLOCKS, tag, (unsigned)vb);
-    g_store(rb + 1 * CHAIN_MAX_BLOCKS, tag, (unsigned)(vb >> 32));
-    g_store(rb + 2 * CHAIN_MAX_BLOCKS, tag, none ? 0xffffffffu : (unsigned)k.row);
-    if (RATIO) g_store(rb + 3 * CHAIN_MAX_BLOCKS, tag, none ? 0xffffffffu : (unsigned)k.t);
+  const unsigned long long vb = (unsigned long long)__double_as_longlong(RATIO ? k.v : k.a);
+  // (granule 3: t, and the stop request in bit 31)
+  const unsigned g3 = (none ? 0x7fffffffu : (unsigned)k.t) | (stopbit << 31);
+  for (int d = 0; d < nd; ++d) {  // every destination (one GPU: nd = 1)
+    gu64* rb = dst(d);
+    if (plane >= 0) g_store<SYS>(rb + (size_t)plane * rs, tag, val);
+    if (RATIO && plane2 >= 0) g_store<SYS>(rb + (size_t)plane2 * rs, tag, val2);
+    if (lane == 0) {
+      g_store<SYS>(rb + 0 * rs, tag, (unsigned)vb);
+      g_store<SYS>(rb + 1 * rs, tag, (unsigned)(vb >> 32));
+      g_store<SYS>(rb + 2 * rs, tag, none ? 0xffffffffu : (unsigned)k.row);
+      if (RATIO) g_store<SYS>(rb + 3 * (size_t)rs, tag, g3);
+    }
   }
 }
 
@@ -386,7 +430,7 @@ __global__ __launch_bounds__(CB) void chain_kernel(
     Key* __restrict__ enter_part, State* st, const Params* __restrict__ prm, int n_ep,
     const double* __restrict__ A, int64_t ld, int64_t m, int64_t N, double* __restrict__ obj,
     Window win, int npiv, int64_t* __restrict__ basis, int64_t* __restrict__ hist,
-    unsigned long long* gr_enter_, unsigned long long* gr_ratio_, int cpb, int rpb, int wp) {
+    unsigned long long* gr_enter_, unsigned long long* gr_ratio_, int cpb, int rpb) {
   static_assert(KMAX <= 32, "slots are lane-indexed and fit the window buffers");
   constexpr int NW = CB / 64;
   constexpr int CH = KMAX % 8 == 0 ? 8 : KMAX % 4 == 0 ? 4 : 2;
@@ -762,7 +806,6 @@ __global__ __launch_bounds__(CB) void chain_kernel(
         tgx = tgx | TAG_ZERO;
       }
       pxl[q] = prhs;
-      if (wp) win.P[(N - 1) * KW + q] = prhs;
     }
     if (ilive && i == r) bas = c;
     rmask |= (i == r) ? (1u << q) : 0u;
@@ -799,13 +842,15 @@ __global__ __launch_bounds__(CB) void chain_kernel(
 #pragma unroll
         for (int x = 1; x < NW; ++x) kmin2(kb, sk[x].v, sk[x].t, sk[x].row, sk[x].a, sk[x].b);
         store_key(enter_part + b, KeyR{kb.v, kb.t, kb.row});
+        // the next window reduces n_ep partials (norm<INIT>'s per-WG count can
+        // exceed B, e.g. 512-thread blocks): the ones past this grid's must not
+        // keep an earlier kernel's keys
+        for (int x = b + B; x < n_ep; x += B) store_key(enter_part + x, keyr_none());
       }
       SPX_PROBE_CHAIN(q, 2);
     }
     // stores for later kernels, after the record (never queued in front of it):
-    // p_q for the register-ring flush variants (wp; the LDS-DMA flush and
-    // row_fix read the records), the pivot's bookkeeping
-    if (wp && jlive) win.P[j * KW + q] = pq;
+    // the pivot's bookkeeping (the flush and row_fix read p from the records)
     if (b == 0 && t == CB - 1) {  // block 0's last thread: not in the polling wave
       st->r = r;
       st->c = c;

@@ -93,9 +93,6 @@ struct Window {
   int32_t* nlist;    // 1             : records in `rec` (reset by lazy_ratio slot 0)
   double* rec;       // N x RECW      : the window's touched columns, compacted by the
                      //                 last lazy_norm: [j | path flags, pad, p_0 .. p_{K-1}]
-  uint32_t* claim;   // nclaim        : flush_dyn_kernel's batch counter per row chunk
-                     //                 (zero between flushes: row_fix_kernel resets them)
-  int nclaim;
 };
 constexpr int RECW = KW + 2;  // doubles per record (272 B)
 
@@ -375,7 +372,10 @@ __global__ __launch_bounds__(BLK) void lazy_norm_kernel(
   // stop: no pivot in this slot (grid-uniform)
   bool stop = status != ST_RUNNING;
   int32_t new_status = ST_RUNNING;
-  if (!stop && (c < 0 || (forced_r < 0 && it >= iter_limit))) {
+  // FIN: a time-limit stop requested through rank 0's payload header
+  bool stop_req = false;
+  if constexpr (FIN) stop_req = (reinterpret_cast<const Key*>(gbuf)->pad >> 32) != 0;
+  if (!stop && (c < 0 || (forced_r < 0 && (it >= iter_limit || stop_req)))) {
     new_status = (c < 0) ? ST_OPTIMAL : ST_LIMIT;
     stop = true;
   }
@@ -510,7 +510,8 @@ template <int KMAX>
 __global__ __launch_bounds__(BLK) void lazy_prep_kernel(
     const Key* __restrict__ ratio_part, const State* st, const Params* __restrict__ prm,
     int n_ratio, int q, const double* __restrict__ A, int64_t ld, int64_t m_local,
-    int64_t row0, int64_t N, Window win, char* __restrict__ sendbuf, int rank) {
+    int64_t row0, int64_t N, Window win, char* __restrict__ sendbuf, int rank,
+    const int32_t* stop_req) {
   static_assert(KMAX <= 64, "slots are lane-indexed");
   constexpr int CH = KMAX % 8 == 0 ? 8 : KMAX % 4 == 0 ? 4 : 2;
   const int lane = threadIdx.x & 63;
@@ -582,226 +583,9 @@ __global__ __launch_bounds__(BLK) void lazy_prep_kernel(
     o.v = have ? k.v : __builtin_inf();
     o.t = have ? k.t : INT64_MAX;
     o.row = have ? k.row : -1;
-    o.pad = rank;
+    o.pad = rank | ((int64_t)stop_requested(rank, stop_req) << 32);  // (spx_kernels.hpp)
     *reinterpret_cast<Key*>(sendbuf) = o;
   }
-}
-
-// ---------------------------------------------------------------------------
-// flush_kernel<K, RT, D, NTS>: apply the window's made pivots to every column
-// tagged with this window's epoch, one streaming read-modify-write pass.
-// grid = rch * G blocks: row chunk of RT*BLK rows x G column groups; group g
-// owns columns g, g+G, ...  Every wave walks its group's columns on its own
-// (no block barrier, no LDS): it reads 64 tags at a time (the next 64 already
-// in flight), takes the tagged columns from the ballot mask (wave-uniform),
-// keeps a ring of D columns' loads in flight, and reads p_s[j] with scalar
-// loads one column ahead, so the update is K x RT pairs of v_mul_f64 /
-// v_add_f64 with an SGPR operand -- no LDS, no readlane.  f_s of the thread's
-// rows stay in registers for the whole launch.
-// Fast path (a full window; column not SPECIAL / ZERO): the straight msub
-// chain for every row, leaving rows included -- row_fix_kernel then rewrites
-// the leaving rows of these columns.  SPECIAL (entered in this window) or ZERO
-// (skip on, some p_s[j] == 0) columns and partial windows take the exact
-// per-element path (apply_pivot), leaving rows included.
-// ---------------------------------------------------------------------------
-// A thread's RT rows of a column: RT = 1: i0; RT = 2: (i0, i0+1); RT = 4: pairs
-// (i0, i0+1) and (i0 + 2*BLK, i0 + 2*BLK + 1), so every wave-instruction moves
-// one contiguous run.  okp[k]: pair k lies inside the local rows (the second
-// row of a pair is < ld, a multiple of 64, so it may be a padding row).
-template <int RT>
-struct Rows {
-  double v[RT];
-};
-template <int RT>
-__device__ __forceinline__ int64_t row_of(int64_t i0, int u) {
-  return i0 + (int64_t)(u >> 1) * 2 * BLK + (u & 1);
-}
-template <int RT>
-constexpr int npairs() { return RT == 1 ? 1 : RT / 2; }
-
-template <int RT, bool NT>
-__device__ __forceinline__ void ld_rows(Rows<RT>& r, const double* p, const bool* okp) {
-  if constexpr (RT == 1) {
-    if (okp[0]) r.v[0] = NT ? __builtin_nontemporal_load(p) : *p;
-  } else {
-#pragma unroll
-    for (int k = 0; k < RT / 2; ++k) {
-      if (okp[k]) {
-        const dbl2 x = ld2<NT>(p + (int64_t)k * 2 * BLK);
-        r.v[2 * k] = x.x;
-        r.v[2 * k + 1] = x.y;
-      }
-    }
-  }
-}
-
-template <int RT, bool NT>
-__device__ __forceinline__ void st_rows(double* p, const Rows<RT>& r, const bool* okp) {
-  if constexpr (RT == 1) {
-    if (okp[0]) {
-      if (NT) __builtin_nontemporal_store(r.v[0], p);
-      else *p = r.v[0];
-    }
-  } else {
-#pragma unroll
-    for (int k = 0; k < RT / 2; ++k)
-      if (okp[k]) st2<NT>(p + (int64_t)k * 2 * BLK, dbl2{r.v[2 * k], r.v[2 * k + 1]});
-  }
-}
-
-struct ColCursor {  // wave-uniform walk over the tagged columns of one group
-  const uint32_t* __restrict__ tag;
-  int64_t g, G, ncol, k0;
-  uint32_t epoch, tg, tgn;
-  uint64_t mask;
-  bool rev;  // walk the group's columns in descending order
-
-  __device__ int64_t col(int64_t k) const { return g + (rev ? ncol - 1 - k : k) * G; }
-  __device__ uint32_t load(int64_t kb, int lane) const {
-    const int64_t k = kb + lane;
-    return (k < ncol) ? tag[col(k)] : 0u;
-  }
-  __device__ void start(int lane) {
-    k0 = 0;
-    tg = load(0, lane);
-    tgn = load(64, lane);
-    mask = __ballot((tg & TAG_EPOCH) == epoch && lane < ncol);
-  }
-  // next tagged column (j, flags); false when the group is exhausted
-  __device__ bool next(int64_t& j, uint32_t& fl, int lane) {
-    while (mask == 0ull) {
-      k0 += 64;
-      if (k0 >= ncol) return false;
-      tg = tgn;
-      tgn = load(k0 + 64, lane);  // the batch after, in flight
-      mask = __ballot((tg & TAG_EPOCH) == epoch && k0 + lane < ncol);
-    }
-    const int bit = __builtin_ctzll(mask);
-    mask &= mask - 1ull;
-    j = col(k0 + bit);
-    fl = (uint32_t)__builtin_amdgcn_readlane((int)tg, bit) & (TAG_SPECIAL | TAG_ZERO);
-    return true;
-  }
-};
-
-template <int K, int RT, int D, bool NTS, bool ALT = false>
-__global__ __launch_bounds__(BLK) void flush_kernel(double* __restrict__ A, int64_t ld,
-                                                    int64_t m_local, int64_t row0, int64_t N,
-                                                    Window win, int npiv, int rch, int G,
-                                                    const Params* __restrict__ prm, State* st,
-                                                    int fmap) {
-  SPX_PROBE(K, 2, 0, true);
-  SPX_PROBE_BLOCK(0);
-  int nm = 0;  // pivots made in this window: a prefix of its npiv slots
-  for (int s = 0; s < npiv; ++s) nm += win.made[s];
-  if (nm == 0) return;
-  const bool full = nm == K;
-  const bool skip = prm->skip_zero != 0;
-  // block -> (row chunk, column group): group-major (consecutive blocks share
-  // a group), chunk-major with fmap bit 0; bit 1 rotates the group by the chunk
-  int chunk = blockIdx.x % rch, g = blockIdx.x / rch;
-  if (fmap & 1) {
-    g = blockIdx.x % G;
-    chunk = blockIdx.x / G;
-  }
-  if (fmap & 2) g = (g + chunk) % G;
-  const int lane = threadIdx.x & 63;
-  const int64_t i0 = (int64_t)chunk * BLK * RT + threadIdx.x * (RT == 1 ? 1 : 2);
-  constexpr int NP = npairs<RT>();
-  bool okp[NP];
-#pragma unroll
-  for (int k = 0; k < NP; ++k) okp[k] = row_of<RT>(i0, 2 * k) < m_local;
-  double f[K][RT];
-#pragma unroll
-  for (int s = 0; s < K; ++s) {
-    Rows<RT> fv{};
-    if (s < nm) ld_rows<RT, false>(fv, win.F + (int64_t)s * ld + i0, okp);
-#pragma unroll
-    for (int u = 0; u < RT; ++u) f[s][u] = fv.v[u];
-  }
-  const double* __restrict__ P = win.P;
-  const uint32_t ep = *win.epoch & TAG_EPOCH;
-  // alternate the sweep direction per window: the columns a flush starts with
-  // are the ones the previous flush wrote last (still in the Infinity Cache)
-  ColCursor cur{win.tag, g, G, (N - g + G - 1) / G, 0, ep, 0u, 0u, 0ull,
-                ALT && (ep & 1u) != 0};
-  cur.start(lane);
-  int64_t touched = 0;
-  int64_t jr[D];
-  uint32_t fr[D];
-  bool hv[D];
-  Rows<RT> t[D];
-#pragma unroll
-  for (int b = 0; b < D; ++b) {
-    hv[b] = cur.next(jr[b], fr[b], lane);  // stays false once the group is exhausted
-    if (hv[b]) ld_rows<RT, false>(t[b], A + jr[b] * ld + i0, okp);
-  }
-  // p_s[j] in SGPRs: K <= 8 keeps the next column's p in flight as well;
-  // larger windows load p in chunks of 16 slots at the column (SGPR budget)
-  constexpr bool PN = K <= 8;
-  constexpr int PCH = K < 16 ? K : 16;
-  double pc[PCH];
-  if (PN && hv[0]) {
-#pragma unroll
-    for (int s = 0; s < PCH; ++s) pc[s] = P[jr[0] * KW + s];
-  }
-  // slots are refilled round-robin, so once one finds the group exhausted every
-  // later one does too: an iteration with hv[0] false has nothing left
-  while (hv[0]) {
-#pragma unroll
-    for (int b = 0; b < D; ++b) {
-      if (!hv[b]) continue;
-      const int bn = (b + 1) % D;
-      double pn[PCH];  // PN: the next column's p, in flight during this update
-      if (PN && hv[bn]) {
-#pragma unroll
-        for (int s = 0; s < PCH; ++s) pn[s] = P[jr[bn] * KW + s];
-      }
-      const int64_t j = jr[b];
-      Rows<RT> x = t[b];
-      const bool fast = full && !fr[b];
-#pragma unroll
-      for (int s0 = 0; s0 < K; s0 += PCH) {
-        if (!PN) {
-#pragma unroll
-          for (int s = 0; s < PCH; ++s) pc[s] = P[j * KW + s0 + s];
-        }
-        if (fast) {
-#pragma unroll
-          for (int s = 0; s < PCH; ++s)
-#pragma unroll
-            for (int u = 0; u < RT; ++u) x.v[u] = msub(x.v[u], f[s0 + s][u], pc[s]);
-        } else {
-#pragma unroll
-          for (int s = 0; s < PCH; ++s) {
-            if (s0 + s < nm) {
-              const int64_t rl = win.r[s0 + s] - row0;
-              const int64_t cs = win.c[s0 + s];
-#pragma unroll
-              for (int u = 0; u < RT; ++u)
-                x.v[u] = apply_pivot(x.v[u], row_of<RT>(i0, u), j, rl, cs, f[s0 + s][u], pc[s],
-                                     skip);
-            }
-          }
-        }
-      }
-      st_rows<RT, NTS>(A + j * ld + i0, x, okp);
-      ++touched;
-      hv[b] = cur.next(jr[b], fr[b], lane);
-      if (hv[b]) ld_rows<RT, false>(t[b], A + jr[b] * ld + i0, okp);
-      if (PN) {
-#pragma unroll
-        for (int s = 0; s < PCH; ++s) pc[s] = pn[s];
-      }
-    }
-  }
-  if (chunk == 0 && threadIdx.x == 0) {
-    atomicAdd(reinterpret_cast<unsigned long long*>(&st->touched_total),
-              (unsigned long long)touched);
-    if (g == 0) st->iters += nm;
-  }
-  SPX_PROBE(K, 2, 1, true);
-  SPX_PROBE_BLOCK(1);
 }
 
 // ---------------------------------------------------------------------------
@@ -1013,263 +797,6 @@ __global__ __launch_bounds__(BLK) void flush_lds_kernel(double* __restrict__ A, 
 }
 
 // ---------------------------------------------------------------------------
-// flush_dyn_kernel<K, D, NTS>: flush_lds_kernel's per-column update with the
-// records handed out dynamically, so every CU works until the list is done.
-//
-// Why: a CU runs 3 flush blocks, and the hardware issues the oldest wave
-// first, so with a static split (records g, g+G, ...) the CU's first block ends
-// ~45 us before its last, which then streams alone with a third of the bytes
-// in flight; CUs also end 16 us apart (profiles/r02/phases_flush_waves.log).
-//
-// How: the records are cut into batches of FB.  Batches 0 and 1 of block g are
-// static (records g*FB.., (G+g)*FB..); later ones are claimed from a per-row-
-// chunk counter (win.claim) with one returning atomic each.  A 5th wave per
-// block is the claimer: it keeps a mailbox of FMB batch bases in LDS ahead of
-// the 4 streaming waves, which read batch bases from LDS only.  So the
-// streaming waves' VMEM order stays exactly one LDS-DMA + one store per column
-// and the constant `s_waitcnt vmcnt` of flush_lds_kernel still retires exactly
-// the slot about to be read (an atomic issued by a streaming wave would join
-// that count).  The arithmetic per element is flush_lds_kernel's, operation for
-// operation; only which block updates a column changes, so the bytes are equal.
-// Every wait is bounded: a wave that waits ~1 s stores ST_FLUSH_FAULT and stops.
-// ---------------------------------------------------------------------------
-constexpr int FB = 8;    // records per batch
-constexpr int FMB = 8;   // mailbox entries (batch ordinals in flight per block)
-constexpr int32_t ST_FLUSH_FAULT = 6;
-constexpr unsigned FLUSH_SPIN_MAX = 1u << 23;
-// LDS words shared by the claimer and the streaming waves: relaxed
-// workgroup-scope atomics (plain ds_read / ds_write, no s_waitcnt of vmcnt;
-// a volatile access would make the compiler drain the wave's VMEM queue)
-__device__ __forceinline__ int lds_ld(int* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-__device__ __forceinline__ void lds_st(int* p, int v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-
-template <int K, int D, bool NTS, bool PART = false>
-__global__ __launch_bounds__(BLK + 64) void flush_dyn_kernel(double* __restrict__ A, int64_t ld,
-                                                             int64_t m_local, int64_t row0,
-                                                             int64_t N, Window win, int npiv,
-                                                             int rch, int G,
-                                                             const Params* __restrict__ prm,
-                                                             State* st, int fmap) {
-  static_assert(D >= 2 && D <= 16 && D + 1 < 2 * FB, "ring depth vs batch size");
-  __shared__ dbl2 ring[NWAVE * D * 64];
-  __shared__ int mbox[FMB];     // record base of batch ordinal n at [n % FMB]; -1: list done
-  __shared__ int produced;      // batch ordinals in the mailbox
-  __shared__ int procb[NWAVE];  // each streaming wave's current batch ordinal (process side)
-  SPX_PROBE(K, 2, 0, true);
-  SPX_PROBE_BLOCK(0);
-  int nm = 0;  // pivots made in this window: a prefix of its npiv slots
-  for (int s = 0; s < npiv; ++s) nm += win.made[s];
-  const int L = *win.nlist;
-  if (nm == 0) return;  // block-uniform
-  const bool full = nm == K;
-  const bool skip = prm->skip_zero != 0;
-  (void)fmap;
-  const int chunk = blockIdx.x % rch, g = blockIdx.x / rch;
-  const int lane = threadIdx.x & 63;
-  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // 0..3 stream, 4 claims
-  if (threadIdx.x == 0) {
-    const int64_t b0 = (int64_t)g * FB, b1 = (int64_t)(G + g) * FB;
-    mbox[0] = b0 < L ? (int)b0 : -1;
-    mbox[1] = (b0 < L && b1 < L) ? (int)b1 : -1;
-    produced = 2;
-  }
-  if (threadIdx.x < NWAVE)
-    procb[threadIdx.x] =
-        (int64_t)chunk * 2 * BLK + (int64_t)threadIdx.x * 128 < m_local ? 0 : 0x7fffffff;
-  __syncthreads();
-  if (chunk == 0 && g == 0 && threadIdx.x == 0) {
-    atomicAdd(reinterpret_cast<unsigned long long*>(&st->touched_total), (unsigned long long)L);
-    st->iters += nm;
-  }
-  if (w == NWAVE) {
-    // ---- the claimer: one lane; batch ordinals 2, 3, ... while there is room ----
-    if (lane != 0 || lds_ld(&mbox[1]) < 0) {
-      if (lane == 0) {  // static batches already end the list
-        lds_st(&mbox[2 % FMB], -1);
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the entry before the count
-        lds_st(&produced, 3);
-      }
-      return;
-    }
-    unsigned spins = 0;
-    for (int n = 2;;) {
-      int minp = lds_ld(&procb[0]);
-#pragma unroll
-      for (int x = 1; x < NWAVE; ++x) minp = min(minp, lds_ld(&procb[x]));
-      // room: the slowest streaming wave no longer reads slot n % FMB (finished
-      // or inactive waves hold 0x7fffffff)
-      if (minp < 0x7fffffff - FMB && n >= minp + FMB) {
-        if (++spins > FLUSH_SPIN_MAX) {
-          st->status = ST_FLUSH_FAULT;
-          lds_st(&mbox[n % FMB], -1);
-          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-          lds_st(&produced, n + 1);
-          return;
-        }
-        __builtin_amdgcn_s_sleep(2);
-        continue;
-      }
-      const unsigned t = __hip_atomic_fetch_add(win.claim + chunk, 1u, __ATOMIC_RELAXED,
-                                                __HIP_MEMORY_SCOPE_AGENT);
-      const int64_t b = (int64_t)(2 * G + (int64_t)t) * FB;
-      const int base = b < L ? (int)b : -1;
-      lds_st(&mbox[n % FMB], base);
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      lds_st(&produced, n + 1);
-      ++n;
-      if (base < 0) return;
-    }
-  }
-  // ---- streaming waves ----
-  const int64_t wrow = (int64_t)chunk * 2 * BLK + (int64_t)w * 128;  // this wave's first row
-  if (wrow >= m_local) return;  // wave-uniform (procb already says "never blocks the claimer")
-  const int64_t i0 = wrow + 2 * lane;
-  const bool ok = i0 < m_local;            // the pair (i0, i0+1) holds local rows
-  const int64_t i0c = ok ? i0 : wrow;      // in-column address for idle lanes
-  double f[K][2];
-#pragma unroll
-  for (int s = 0; s < K; ++s) {
-    dbl2 fv = dbl2{0.0, 0.0};
-    if (s < nm && ok) fv = ld2<false>(win.F + (int64_t)s * ld + i0);
-    f[s][0] = fv.x;
-    f[s][1] = fv.y;
-  }
-  typedef const __attribute__((address_space(4))) double cdbl;
-  typedef const __attribute__((address_space(4))) int64_t ci64;
-  cdbl* rec = (cdbl*)win.rec;
-  ci64* hdr = (ci64*)win.rec;
-  ci64* wr = (ci64*)win.r;
-  ci64* wc = (ci64*)win.c;
-  const uint32_t lds0 =
-      (uint32_t)(uintptr_t)((__attribute__((address_space(3))) dbl2*)&ring[0]) +
-      (uint32_t)(w * D * 64) * (uint32_t)sizeof(dbl2);
-  bool fault = false;
-  // batch ordinal n's record base (the claimer may still be on it: bounded wait)
-  auto batch = [&](int n) -> int {
-    unsigned spins = 0;
-    while (__builtin_amdgcn_readfirstlane(lds_ld(&produced)) <= n) {
-      if (++spins > FLUSH_SPIN_MAX) {
-        fault = true;
-        return -1;
-      }
-      __builtin_amdgcn_s_sleep(1);
-    }
-    asm volatile("" ::: "memory");  // the entry is read after the count
-    return __builtin_amdgcn_readfirstlane(lds_ld(&mbox[n % FMB]));
-  };
-  auto blen = [&](int base) -> int { return base < 0 ? 0 : min(FB, L - base); };
-  // issue cursor (LDS-DMA side, D + 1 columns ahead) and process cursor
-  int ni = 0, ib = batch(0), io = 0, il = blen(ib);
-  auto issue_next = [&]() -> int {  // record index at the issue cursor (then advance); -1: done
-    if (ib < 0) return -1;
-    const int r = ib + io;
-    if (++io == il) {
-      ib = batch(++ni);
-      io = 0;
-      il = blen(ib);
-    }
-    return r;
-  };
-  int np = 0, pb = ib, po = 0, pl = il;
-  auto proc_next = [&]() -> int {  // advance the process cursor; its record index or -1
-    if (++po == pl) {
-      ++np;
-      if (lane == 0) lds_st(&procb[w], np);  // ordinals < np are free for the claimer
-      asm volatile("" ::: "memory");
-      pb = __builtin_amdgcn_readfirstlane(lds_ld(&mbox[np % FMB]));  // the issue side passed it
-      po = 0;
-      pl = blen(pb);
-    }
-    return pb < 0 ? -1 : pb + po;
-  };
-  const int r0 = issue_next();
-  if (r0 < 0) {
-    if (lane == 0) lds_st(&procb[w], 0x7fffffff);
-    if (fault) st->status = ST_FLUSH_FAULT;
-    return;
-  }
-#pragma unroll
-  for (int s = 0; s < K; ++s) asm volatile("" ::"v"(f[s][0]), "v"(f[s][1]));
-  wait_vmcnt<0>();
-  // prologue: columns 0..D-1 (dummy re-reads of the last real column past the end)
-  const double* last_src = A + (hdr[(int64_t)r0 * RECW] & 0xffffffffll) * ld + i0c;
-  glds16(last_src, lds0);
-#pragma unroll
-  for (int d = 1; d < D; ++d) {
-    const int rd = issue_next();
-    if (rd >= 0) last_src = A + (hdr[(int64_t)rd * RECW] & 0xffffffffll) * ld + i0c;
-    glds16(last_src, lds0 + (uint32_t)(d * 64 * sizeof(dbl2)));
-  }
-  int rn = issue_next();                                  // column D (next DMA)
-  int64_t hn = rn >= 0 ? hdr[(int64_t)rn * RECW] : 0;
-  int64_t hc = hdr[(int64_t)r0 * RECW];                   // the column being updated
-  double pc[K];
-#pragma unroll
-  for (int s = 0; s < K; ++s) pc[s] = rec[(int64_t)r0 * RECW + 2 + s];
-  int cols = 0;
-  for (int k = 0;; ++k) {
-    const int slot = k % D;
-    if (k >= D - 1) wait_vmcnt<2 * (D - 1)>();
-    else wait_vmcnt<D - 1>();
-    dbl2 x = ring[(w * D + slot) * 64 + lane];
-    const int64_t j = hc & 0xffffffffll;
-    if ((hc >> 32) == 0 && (PART || full)) {
-      if constexpr (!PART) {
-#pragma unroll
-        for (int s = 0; s < K; ++s) {
-          x.x = msub(x.x, f[s][0], pc[s]);
-          x.y = msub(x.y, f[s][1], pc[s]);
-        }
-      } else {
-#pragma unroll
-        for (int s = 0; s < K; ++s) {
-          if (s < nm) {
-            x.x = msub(x.x, f[s][0], pc[s]);
-            x.y = msub(x.y, f[s][1], pc[s]);
-          }
-        }
-      }
-    } else {
-      ci64* wrk = wr;
-      ci64* wck = wc;
-      asm volatile("" : "+s"(wrk), "+s"(wck));
-#pragma unroll
-      for (int s = 0; s < K; ++s) {
-        if (s < nm) {
-          const int64_t rl = wrk[s] - row0;
-          const int64_t cs = wck[s];
-          x.x = apply_pivot(x.x, i0, j, rl, cs, f[s][0], pc[s], skip);
-          x.y = apply_pivot(x.y, i0 + 1, j, rl, cs, f[s][1], pc[s], skip);
-        }
-      }
-    }
-    if (ok) st2<NTS>(A + j * ld + i0, x);
-    ++cols;
-    // DMA of column k + D into the slot just read (a dummy re-read past the end)
-    if (rn >= 0) last_src = A + (hn & 0xffffffffll) * ld + i0c;
-    glds16(last_src, lds0 + (uint32_t)(slot * 64 * sizeof(dbl2)));
-    const int rk = proc_next();  // column k + 1
-    if (rk < 0) break;
-    hc = hdr[(int64_t)rk * RECW];
-#pragma unroll
-    for (int s = 0; s < K; ++s) pc[s] = rec[(int64_t)rk * RECW + 2 + s];
-    rn = issue_next();  // column k + D + 1
-    hn = rn >= 0 ? hdr[(int64_t)rn * RECW] : 0;
-  }
-  wait_vmcnt<0>();  // no DMA may land in LDS after the wave has exited
-  if (lane == 0) lds_st(&procb[w], 0x7fffffff);
-  if (fault) st->status = ST_FLUSH_FAULT;
-  SPX_PROBE_WAVE(w, cols);
-  (void)cols;
-  SPX_PROBE(K, 2, 1, true);
-  SPX_PROBE_BLOCK(1);
-}
-
-// ---------------------------------------------------------------------------
 // row_fix_kernel<K>: after a window's flush (its made slots: a prefix of K),
 // rewrite the leaving rows of the fast-path columns (the window's records
 // without SPECIAL / ZERO flags; p values from the records).  For such a column no
@@ -1285,10 +812,6 @@ __global__ __launch_bounds__(BLK) void row_fix_kernel(double* __restrict__ A, in
   __shared__ double fr[K][K];  // fr[L][s] = f_s[r_L]
   __shared__ int64_t rows[K];
   __shared__ int lastL[K];
-  // the flush's batch counters start at zero for the next window (this kernel
-  // follows every flush on the stream)
-  if (blockIdx.x == 0)
-    for (int t = threadIdx.x; t < win.nclaim; t += BLK) win.claim[t] = 0u;
   // one thread per record of the window (the flush's compacted list: column,
   // path flags, p_0..p_{K-1}); all loads are independent: issue them together
   const int kr = blockIdx.x * BLK + threadIdx.x;

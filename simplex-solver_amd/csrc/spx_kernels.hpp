@@ -342,7 +342,11 @@ __global__ __launch_bounds__(BLK) void norm_kernel(const double* __restrict__ A,
   int64_t r = -1;
   const double* __restrict__ pw = nullptr;  // FINISH: the winner's p row
   if (MODE == MODE_FUSED || MODE == MODE_FINISH) {
-    if (c < 0 || (forced_r < 0 && it >= prm->iter_limit)) {
+    // FINISH: a time-limit stop requested by rank 0's host rides in rank 0's
+    // payload header, so every rank stops before the same pivot
+    const bool stop_req =
+        MODE == MODE_FINISH && (reinterpret_cast<const Key*>(gbuf)->pad >> 32) != 0;
+    if (c < 0 || (forced_r < 0 && (it >= prm->iter_limit || stop_req))) {
       if (blockIdx.x == 0 && threadIdx.x == 0) st->status = (c < 0) ? ST_OPTIMAL : ST_LIMIT;
       return;
     }
@@ -444,6 +448,15 @@ __global__ __launch_bounds__(BLK) void norm_kernel(const double* __restrict__ A,
   }
 }
 
+// Time-limit stop of a sharded solve (spx_solve): rank 0's host sets a word of
+// pinned host memory; rank 0's payload header carries it (Key.pad bit 32) to
+// every rank, which stop before the same pivot (status ST_LIMIT).
+__device__ __forceinline__ bool stop_requested(int rank, const int32_t* stop_req) {
+  return rank == 0 && stop_req &&
+         __hip_atomic_load(const_cast<int32_t*>(stop_req), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM) != 0;
+}
+
 // prep_kernel (sharded rank): this rank's leaving-row candidate for the
 // pending pivot and its normalised row, packed as the all-gather payload
 // [Key (pad = rank) | p[0..N)].  One thread per column.  A forced pivot
@@ -453,7 +466,8 @@ __global__ __launch_bounds__(BLK) void prep_kernel(const double* __restrict__ A,
                                                    const double* __restrict__ F2,
                                                    const Key* __restrict__ ratio_part,
                                                    char* __restrict__ sendbuf, int rank,
-                                                   const State* st) {
+                                                   const State* st,
+                                                   const int32_t* stop_req) {
   const bool live = st->status == ST_RUNNING && st->c_next >= 0;
   const int64_t forced_r = st->forced_r;
   KeyR k = keyr_none();
@@ -474,7 +488,7 @@ __global__ __launch_bounds__(BLK) void prep_kernel(const double* __restrict__ A,
     o.v = k.v;
     o.t = k.t;
     o.row = live ? k.row : -1;
-    o.pad = rank;
+    o.pad = rank | ((int64_t)stop_requested(rank, stop_req) << 32);
     if (!live) {
       o.v = __builtin_inf();
       o.t = INT64_MAX;

@@ -103,6 +103,8 @@ SIGNATURES = {
     "spx_chain_timing": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_double),
                                         ctypes.POINTER(ctypes.c_int64), ctypes.c_int]),
     "spx_get_chain": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_int)]),
+    "spx_set_chain_budget": (ctypes.c_int, [ctypes.c_int, ctypes.c_int]),
+    "spx_get_chain_stats": (ctypes.c_int, [_P, _LP]),
     "spx_get_elim_variant": (ctypes.c_int, [_P, _LP]),
     "spx_get_flush_variant": (ctypes.c_int, [_P, _LP]),
     "spx_set_elim_variant": (ctypes.c_int, [_P, ctypes.c_int, ctypes.c_int, ctypes.c_int,

@@ -88,7 +88,7 @@ class DeviceTableau:
     def __init__(self, device: int = 0, *, _sharded=None):
         self._lib = L.lib()
         self._ctx = ctypes.c_void_p()
-        self.sharded = _sharded is not None  # row shards reject windows (spx_set_window)
+        self.sharded = _sharded is not None
         if _sharded is None:
             rc = self._lib.spx_create(ctypes.byref(self._ctx), int(device))
         else:
@@ -327,6 +327,22 @@ class DeviceTableau:
         self._check(self._lib.spx_get_chain(self._ctx, ctypes.byref(b)), "spx_get_chain")
         return int(b.value)
 
+    def chain_stats(self) -> dict:
+        """Admission record: calls run with the persistent chain, calls refused
+        (launch-per-phase chain instead), blocks held now (spx_get_chain_stats)."""
+        out = np.zeros(3, dtype=np.int64)
+        self._check(self._lib.spx_get_chain_stats(self._ctx, _lptr(out)), "spx_get_chain_stats")
+        return {"persistent_calls": int(out[0]), "refused_calls": int(out[1]),
+                "blocks_held": int(out[2])}
+
+    @staticmethod
+    def set_chain_budget(device: int, blocks: int) -> None:
+        """Process-wide budget of persistent-chain blocks in flight on `device`
+        (-1: default = the CU count or SPX_CHAIN_BUDGET; 0: never persistent)."""
+        rc = L.lib().spx_set_chain_budget(int(device), int(blocks))
+        if rc < 0:
+            raise SpxError(f"spx_set_chain_budget failed ({rc})")
+
     def set_ld_pad(self, pad: int) -> None:
         """Extra doubles per stored column, applied at the next load."""
         self._check(self._lib.spx_set_ld_pad(self._ctx, int(pad)), "spx_set_ld_pad")
@@ -339,11 +355,10 @@ class DeviceTableau:
         R: rows per thread (2/4/8, 0 auto); target_wgs: grid target (0 auto);
         nt_flags: non-temporal bit 0 loads, bit 1 stores (-1 auto).  The C
         `interleave` word packs: bit 0 interleaved columns, bit 1 pipelining
-        OFF, bit 2 XCD-aware swizzle, bits 8-10 window flush variant (0 the
-        LDS-DMA ring of 12, 6/7 rings of 9/10, 1-5 register rings for
-        power-of-two K), bits 11-13 flush block map (bit 11 chunk-major, bit 12
-        groups rotated by row chunk; 4 = bit 13: the LDS-DMA flush claims its
-        columns dynamically, block map ignored).  Pass `interleave` to set the whole word,
+        OFF, bit 2 XCD-aware swizzle, bits 8-10 window flush variant (only 0,
+        the LDS-DMA ring, remains; others raise), bits 11-12 flush block map
+        (bit 11 chunk-major, bit 12 groups rotated by row chunk; bit 13, the
+        removed dynamic-claim flush, raises).  Pass `interleave` to set the whole word,
         or leave it None and give only the keyword fields to change: the others
         keep their current values (read back with elim_variant())."""
         if interleave is None:

@@ -1,0 +1,129 @@
+"""Full-size solve fixtures: the C oracle (oracle/spx_oracle.c) run to
+optimality on BASELINE.json config 3 (8192 x 8192 dense LP, Dantzig) and
+config 5 (4096 x 4096 degenerate LP, Bland), plus HiGHS's objective on the same
+LP (scipy.optimize.linprog(method='highs-ds'), the reference's answer path at
+app/controllers/solver_controller.py:76-85).
+
+TEST INFRASTRUCTURE: run once in the dev container (no GPU needed); writes
+tests/golden/fullsize_<name>.npz (the whole (r, c) pivot sequence and the final
+basis, compressed) and tests/golden/fullsize.json (pivot count, objective,
+SHA-256 digests of the final tableau bytes and of checkpoints along the way,
+HiGHS objective / status / time).  tests/test_gpu_fullsize.py solves the same
+LPs on the GPU through the C-ABI and compares every index, the basis, the
+digests and the objective.
+
+Usage:  python tests/golden/make_fullsize.py [config3|config5|highs3|highs5 ...]
+"""
+from __future__ import annotations
+
+import hashlib
+import json
+import os
+import sys
+import time
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, os.path.join(ROOT, "simplex-solver_amd"))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+
+from oracle import c_oracle as C  # noqa: E402
+from simplex_amd import synth  # noqa: E402
+
+JSON = os.path.join(HERE, "fullsize.json")
+
+# the configs (seeds as bench.py / tools/bench_configs.py use them)
+CONFIGS = {
+    "config3": dict(kind="dense", m=8192, n=8192, seed=20251205, rule="dantzig",
+                    checkpoints=[24, 240, 2400]),
+    "config5": dict(kind="degenerate", m=4096, n=4096, seed=5, rule="bland",
+                    checkpoints=[24, 240, 2400]),
+}
+
+
+def digest(T: np.ndarray) -> str:
+    """SHA-256 of the row-major (m+1) x N float64 tableau bytes (objective row last)."""
+    return hashlib.sha256(np.ascontiguousarray(T).tobytes()).hexdigest()
+
+
+def load_json() -> dict:
+    if os.path.exists(JSON):
+        with open(JSON) as f:
+            return json.load(f)
+    return {}
+
+
+def save_json(d: dict) -> None:
+    tmp = JSON + ".tmp"
+    with open(tmp, "w") as f:
+        json.dump(d, f, indent=1, sort_keys=True)
+        f.write("\n")
+    os.replace(tmp, JSON)
+
+
+def oracle_solve(name: str) -> dict:
+    cfg = CONFIGS[name]
+    T, basis = synth.full_tableau(cfg["kind"], cfg["m"], cfg["n"], cfg["seed"])
+    hist: list = []
+    cps = {}
+    t0 = time.perf_counter()
+    chunk = 24
+    status = 1
+    while status == 1:
+        nxt = min([k for k in cfg["checkpoints"] if k > len(hist)] or [len(hist) + 2400])
+        want = min(chunk, nxt - len(hist))
+        status, h = C.solve(T, basis, rule=cfg["rule"], max_iters=want, hist_cap=want)
+        hist += h
+        if len(hist) in cfg["checkpoints"] and status == 1:
+            cps[str(len(hist))] = digest(T)
+        if len(hist) % 2400 < chunk:
+            print(f"{name}: {len(hist)} pivots, {time.perf_counter() - t0:.0f} s, "
+                  f"z = {T[-1, -1]!r}", flush=True)
+        chunk = 240
+    el = time.perf_counter() - t0
+    h = np.asarray(hist, dtype=np.int32).reshape(-1, 2)
+    np.savez_compressed(os.path.join(HERE, f"fullsize_{name}.npz"), hist=h,
+                        basis=basis.astype(np.int32))
+    out = dict(cfg, status=int(status), pivots=len(hist), objective=float(T[-1, -1]),
+               objective_hex=float(T[-1, -1]).hex(), tableau_sha256=digest(T),
+               checkpoint_sha256=cps, oracle_seconds=el, oracle_threads=C.threads(),
+               generator="tests/golden/make_fullsize.py (oracle/spx_oracle.c, skip_zero)")
+    print(f"{name}: status {status}, {len(hist)} pivots in {el:.0f} s, z = {T[-1, -1]!r}",
+          flush=True)
+    return out
+
+
+def highs(name: str, time_limit: float = 3000.0) -> dict:
+    from scipy.optimize import linprog
+    cfg = CONFIGS[name]
+    A, b, c = synth.lp_data(cfg["kind"], cfg["m"], cfg["n"], cfg["seed"])
+    t0 = time.perf_counter()
+    r = linprog(-c, A_ub=A, b_ub=b, bounds=[(0, None)] * cfg["n"], method="highs-ds",
+                options={"presolve": True, "time_limit": time_limit})
+    el = time.perf_counter() - t0
+    out = dict(highs_status=int(r.status), highs_message=str(r.message),
+               highs_objective=(float(-r.fun) if r.fun is not None else None),
+               highs_nit=int(getattr(r, "nit", -1)), highs_seconds=el,
+               highs_method="highs-ds (scipy %s)" % __import__("scipy").__version__)
+    print(name, out, flush=True)
+    return out
+
+
+def main(argv):
+    todo = argv or ["config3", "config5", "highs3", "highs5"]
+    for what in todo:
+        if what.startswith("highs"):
+            name = "config" + what[5:]
+            res = highs(name)
+        else:
+            name = what
+            res = oracle_solve(name)
+        d = load_json()
+        d.setdefault(name, {}).update(res)
+        save_json(d)
+
+
+if __name__ == "__main__":
+    main(sys.argv[1:])

@@ -62,6 +62,26 @@ def test_chain_matches_lazy_chain_and_oracle(eng_cls, K, shape, rule, mode):
     assert np.array_equal(out, ref) and np.array_equal(b, rb)
 
 
+@pytest.mark.parametrize("K", [4, 8])
+def test_chain_512_threads_no_stale_entering_partials(eng_cls, K):
+    """512-thread chain blocks: B = ceil((N-1)/512) blocks, but the window's
+    first pivot reduces max(4 * ceil(N/256), B) entering partials.  Every
+    window after the first must see only the previous chain's keys: here the
+    most negative reduced costs sit in the upper column blocks (whose initial
+    keys a stale partial would keep), so a stale key would re-pick a column
+    that already entered (spx_chain.hpp)."""
+    T, basis = _random_tableau(301, 2051, seed=91)
+    n = 2051 - 1 - 300
+    T[300, 1280:n] = -10.0 - 1e-3 * np.arange(n - 1280)
+    kw = dict(max_iters=6 * K + 3)
+    res, h, out, b, blocks = _run(eng_cls, T, basis, K, 3, **kw)
+    assert blocks == 5
+    ref, rb = T.copy(), basis.copy()
+    st, hist = O.solve_tableau(ref, rb, max_iters=6 * K + 3)
+    assert [tuple(x) for x in h] == hist and res.status == st
+    assert np.array_equal(out, ref) and np.array_equal(b, rb)
+
+
 @pytest.mark.parametrize("mode", [0])
 @pytest.mark.parametrize("min_blocks", [0, 3, 64, 100, 256])
 def test_chain_grid_sizes_bit_exact(eng_cls, min_blocks, mode):
@@ -174,6 +194,68 @@ def test_chain_concurrent_contexts(eng_cls):
     ref = _run(eng_cls, T, basis, 24, 1, max_iters=100)
     for r in res:
         assert r[1] == ref[1] and r[2].tobytes() == ref[2].tobytes()
+
+
+def test_chain_admission_more_chains_than_cus(eng_cls):
+    """Six windowed contexts at config-3 width (64 chain blocks each: 384 >
+    256 CUs) solving from six threads at once.  The process admits persistent
+    chains only while their blocks fit the CUs; the others run the
+    launch-per-phase chain.  Every context must finish byte-identical to a
+    sequential run (no SPX_E_STATE from a partly resident chain)."""
+    T, basis = _random_tableau(257, 16385, seed=61)
+    kw = dict(max_iters=120)
+    ref = _run(eng_cls, T, basis, 24, 0, **kw)
+    assert ref[4] == 64
+    res, stats, errs = [None] * 6, [None] * 6, []
+    barrier = threading.Barrier(6)
+
+    def work(k):
+        try:
+            with eng_cls(0) as e:
+                e.set_window(24)
+                e.load(T, basis)
+                barrier.wait()
+                for _ in range(3):  # several calls per context: admission per call
+                    e.solve(max_iters=40)
+                res[k] = (e.history().tolist(), e.tableau().tobytes())
+                stats[k] = e.chain_stats()
+        except Exception as ex:  # noqa: BLE001 - reported below
+            errs.append(repr(ex))
+
+    th = [threading.Thread(target=work, args=(k,)) for k in range(6)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    assert not errs, errs
+    for r in res:
+        assert r[0] == ref[1] and r[1] == ref[2].tobytes()
+    assert sum(s["persistent_calls"] + s["refused_calls"] for s in stats) == 18
+    assert all(s["blocks_held"] == 0 for s in stats)
+
+
+def test_chain_budget_zero_runs_launch_per_phase(eng_cls):
+    """spx_set_chain_budget(device, 0): every call is refused the persistent
+    chain and runs the launch-per-phase chain, with the same bytes."""
+    T, basis = _random_tableau(300, 900, seed=62)
+    ref = _run(eng_cls, T, basis, 16, 0, max_iters=50)
+    eng_cls.set_chain_budget(0, 0)
+    try:
+        with eng_cls(0) as e:
+            e.set_window(16)
+            e.load(T, basis)
+            e.solve(max_iters=50)
+            out, h, st = e.tableau(), e.history().tolist(), e.chain_stats()
+    finally:
+        eng_cls.set_chain_budget(0, -1)
+    assert st["persistent_calls"] == 0 and st["refused_calls"] == 1
+    assert h == ref[1] and out.tobytes() == ref[2].tobytes()
+    with eng_cls(0) as e:  # default budget again: admitted
+        e.set_window(16)
+        e.load(T, basis)
+        e.run_pivots(32)
+        e.sync()
+        assert e.chain_stats()["persistent_calls"] == 1
 
 
 def test_chain_set_validated(eng_cls):

@@ -365,6 +365,31 @@ def test_sharded_virtual_ranks_bit_exact(world, kind, m, n, rule):
         assert np.array_equal(b, basis)
 
 
+@pytest.mark.parametrize("window", [0, 8])
+def test_sharded_time_limit_stops_every_rank_at_one_pivot(window):
+    """time_limit on row shards (the reference always passes time_limit 10,
+    solver_controller.py:76): rank 0's host asks its device to stop, its
+    payload header carries the request, and every rank stops before the same
+    pivot with status 1 (iteration / time limit), bit-exact to the oracle
+    after that many pivots."""
+    from simplex_amd import synth
+    m, n = 600, 900
+    outs = _sharded_threads(3, "dense", m, n, 5, "dantzig", window=window, time_limit=1e-4)
+    T, basis = synth.full_tableau("dense", m, n, 5)
+    _, full = O.solve_tableau(T.copy(), basis.copy(), max_iters=200000)
+    iters = {res.iters for (_, _, res, _, _, _) in outs.values()}
+    hists = {tuple(map(tuple, h)) for (_, _, _, h, _, _) in outs.values()}
+    assert len(iters) == 1 and len(hists) == 1
+    k = iters.pop()
+    assert 0 < k < len(full)
+    st, hist = O.solve_tableau(T, basis, max_iters=k)
+    for rank, (r0, r1, res, h, Tl, b) in outs.items():
+        assert res.status == 1
+        assert [tuple(x) for x in h] == hist
+        assert np.array_equal(Tl[:-1], T[r0:r1]) and np.array_equal(Tl[-1], T[-1])
+        assert np.array_equal(b, basis)
+
+
 def test_run_pivots_timed_graph_matches_untimed(eng_cls):
     """bench.py's timed region (one hipGraph with event nodes around every
     elimination) computes exactly what the plain pivot loop computes."""

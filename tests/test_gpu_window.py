@@ -57,25 +57,24 @@ def test_window_rule_pivots_bit_exact(eng_cls, K, shape, skip):
     assert out.tobytes() == out0.tobytes()
 
 
-def _set_flush_variant(e, fv):
-    """fv = flush variant (bits 0-2) + 8 * block map (bits 3-4)."""
-    e.set_elim_variant(0, 0, -1, flush_variant=fv & 7, flush_map=fv >> 3)
+def _set_flush_map(e, fmap):
+    """fmap = flush block map (bit 0 chunk-major, bit 1 groups rotated by chunk)."""
+    e.set_elim_variant(0, 0, -1, flush_map=fmap)
     v = e.elim_variant()
-    assert (v["flush_var"], v["flush_map"]) == (fv & 7, fv >> 3)
+    assert (v["flush_var"], v["flush_map"]) == (0, fmap)
 
 
-@pytest.mark.parametrize("fv", list(range(8)) + [8, 16, 24, 14, 32, 33])
+@pytest.mark.parametrize("fmap", [0, 1, 2, 3])
 @pytest.mark.parametrize("K", [2, 12, 16, 24, 32])
 @pytest.mark.parametrize("shape", [(17, 40), (700, 1500), (1537, 2600)])
-def test_window_flush_variants_bit_exact(eng_cls, fv, K, shape):
-    """Every flush kernel variant (register rings of 1/2/4 rows per lane, the
-    LDS-DMA ring over compacted records) and block map (fv >> 3: chunk-major,
+def test_window_flush_block_maps_bit_exact(eng_cls, fmap, K, shape):
+    """The LDS-DMA flush under every block map (group-major, chunk-major,
     rotated groups) gives the single-pivot bytes."""
-    T, basis = _random_tableau(*shape, seed=shape[0] + 3 * shape[1] + fv)
+    T, basis = _random_tableau(*shape, seed=shape[0] + 3 * shape[1] + fmap)
     with eng_cls(0) as e:
         e.set_window(K)
         e.load(T, basis)
-        _set_flush_variant(e, fv)
+        _set_flush_map(e, fmap)
         res = e.solve(max_iters=3 * K + 5)
         h, out = e.history().tolist(), e.tableau()
     with eng_cls(0) as s:
@@ -84,6 +83,17 @@ def test_window_flush_variants_bit_exact(eng_cls, fv, K, shape):
         assert h == s.history().tolist()
         assert res.status == res0.status and res.iters == res0.iters
         assert out.tobytes() == s.tableau().tobytes()
+
+
+def test_removed_flush_variants_rejected(eng_cls):
+    """The register-ring (1-5), ring-9/10 (6/7) and dynamically claimed flushes
+    measured slower and were removed: selecting one is an error."""
+    with eng_cls(0) as e:
+        for fv in (1, 5, 6, 7):
+            with pytest.raises(Exception):
+                e.set_elim_variant(0, 0, -1, flush_variant=fv)
+        with pytest.raises(Exception):
+            e.set_elim_variant(0, 0, -1, flush_map=4)
 
 
 @pytest.mark.parametrize("K", [4, 16])

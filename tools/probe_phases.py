@@ -32,7 +32,7 @@ def main():
     ap.add_argument("--m", type=int, default=8192)
     ap.add_argument("--n", type=int, default=8192)
     ap.add_argument("--build-only", action="store_true")
-    ap.add_argument("--fv", type=int, default=0)
+    ap.add_argument("--fmap", type=int, default=0)
     ap.add_argument("--chain", type=int, default=0, help="0 persistent chain, 1 lazy kernels")
     a = ap.parse_args()
     if a.build_only or not os.path.exists(LIB):
@@ -49,7 +49,7 @@ def main():
     e.set_window(K)
     e.set_chain(a.chain)
     e.load_rows(Tf, obj, basis, a.m, 0)
-    e.set_elim_variant(0, 0, -1, flush_variant=a.fv & 7, flush_map=a.fv >> 3)
+    e.set_elim_variant(0, 0, -1, flush_map=a.fmap & 3)
     del Tf
     e.run_pivots(4 * K)
     e.sync()
