@@ -108,6 +108,30 @@ int spx_create_sharded(spx_ctx** out, int device, int rank, int nranks, const ch
 int spx_create_sharded_local(spx_ctx** out, int device, int rank, int nranks,
                              const char id[128]);
 
+/* Like spx_create_sharded, but with no communicator: the ranks (processes or
+ * threads, on one or several GPUs, at most 16) exchange only through the
+ * row-sharded persistent chain set up by spx_peer_export / spx_peer_import, so
+ * such a context must run windowed (spx_set_window) with the persistent chain. */
+int spx_create_sharded_peer(spx_ctx** out, int device, int rank, int nranks);
+
+/* ---- row-sharded persistent chain -------------------------- */
+/* After every rank loaded its rows, the ranks' windows can run ONE persistent
+ * launch per window (the single-GPU chain, spx_chain.hpp) instead of three
+ * launches and an RCCL all-gather per pivot: each block's ratio record is
+ * written to every rank's record buffer and polled locally, and the leaving
+ * row's stale values are read from its owner's tableau through a peer
+ * pointer.  Across processes the peers are IPC-mapped: spx_peer_export writes
+ * this rank's blob (spx_peer_blob_size() bytes), the caller all-gathers the
+ * blobs (e.g. torch.distributed over gloo) and every rank calls
+ * spx_peer_import with all of them in rank order.  Virtual ranks of one
+ * process call spx_peer_chain_local instead.  Valid until the next load; the
+ * chain is used when its grid fits (every rank's blocks in one poll, the
+ * chains sharing a GPU all resident), else the RCCL path runs. */
+int spx_peer_blob_size(void);
+int spx_peer_export(spx_ctx* ctx, void* out, int64_t cap);
+int spx_peer_import(spx_ctx* ctx, const void* blobs, int nranks);
+int spx_peer_chain_local(spx_ctx* ctx);
+
 /* ---- data in / out ------------------------------------------------------- */
 /* Load a full tableau of `rows` = m+1 rows (objective row LAST) and `cols` = N
  * columns; basis has m entries.  ld is the host leading dimension. */

@@ -146,6 +146,13 @@ struct spx_ctx {
   bool chain_denied = false;
   int64_t chain_calls[2] = {0, 0};  // calls run with the persistent / the lazy chain
 
+  // row-sharded persistent chain: every rank's ratio-record
+  // buffer and stale tableau, valid for the loaded tableau (spx_peer_*)
+  bool peer_ok = false;
+  ChainPeers peers{};
+  std::vector<void*> ipc_open;  // IPC-mapped peer buffers (closed on reload / destroy)
+  int peer_same_dev = 1;        // ranks whose chains share this rank's GPU
+
   // graph cache
   hipGraphExec_t gexec = nullptr;
   int gchunk = 0;
@@ -201,8 +208,17 @@ void drop_graphs(spx_ctx* ctx) {
   ctx->gchunk = 0;
 }
 
+void close_peers(spx_ctx* ctx) {
+  for (void* p : ctx->ipc_open) (void)hipIpcCloseMemHandle(p);
+  ctx->ipc_open.clear();
+  ctx->peer_ok = false;
+  ctx->peers = ChainPeers{};
+  ctx->peer_same_dev = 1;
+}
+
 int free_buffers(spx_ctx* ctx) {
   drop_graphs(ctx);
+  close_peers(ctx);
   dfree(ctx->A);
   dfree(ctx->obj);
   dfree(ctx->F);
@@ -399,21 +415,29 @@ int lazy_ratio_grid(const spx_ctx* ctx) {
 // 512-thread blocks; automatic: 256 threads (measured faster than 512 at
 // config 3, profiles/r02), 512 when the tableau needs more than 256 blocks.
 int chain_blocks(spx_ctx* ctx, int* cb_out = nullptr, bool ignore_admission = false) {
-  if (ctx->sharded || ctx->chain_mode == 1) return 0;
+  if (ctx->chain_mode == 1) return 0;
+  if (ctx->sharded && !ctx->peer_ok) return 0;  // shards: only once the peers are known
   if (ctx->chain_denied && !ignore_admission) return 0;
   if (!ctx->n_cu) {
     (void)hipDeviceGetAttribute(&ctx->n_cu, hipDeviceAttributeMultiprocessorCount, ctx->device);
     if (ctx->n_cu <= 0) ctx->n_cu = 256;
   }
-  const int64_t wide = std::max<int64_t>(ctx->N, ctx->m_local);
+  // row shards: one grid geometry on every rank (B from the largest row
+  // block), so every rank decides the same way
+  const int64_t rows =
+      ctx->sharded ? (ctx->m_global + ctx->nranks - 1) / ctx->nranks : ctx->m_local;
+  const int64_t wide = std::max<int64_t>(ctx->N, rows);
   const int cb = ctx->chain_mode == 2 ? 256 : ctx->chain_mode == 3 ? 512
                  : (wide > 256 * std::min(ctx->n_cu, CHAIN_MAX_BLOCKS) ? 512 : 256);
   if (cb_out) *cb_out = cb;
   // the N-1 candidate columns set the width: the RHS column rides along with
   // the last block's last thread when B * cpb == N - 1 (spx_chain.hpp, xown)
-  const int64_t need = std::max<int64_t>({(ctx->N - 1 + cb - 1) / cb, (ctx->m_local + cb - 1) / cb,
+  const int64_t need = std::max<int64_t>({(ctx->N - 1 + cb - 1) / cb, (rows + cb - 1) / cb,
                                           1, (int64_t)ctx->chain_min_blocks});
   const int64_t cap = std::min<int64_t>((int64_t)ctx->n_cu, CHAIN_MAX_BLOCKS);
+  if (ctx->sharded)  // every rank's records in one poll; the chains sharing a GPU all resident
+    return need * ctx->nranks <= CHAIN_SH_SLOTS && need * ctx->peer_same_dev <= cap ? (int)need
+                                                                                      : 0;
   return need <= cap ? (int)need : 0;
 }
 
@@ -449,6 +473,9 @@ int adm_budget_locked(ChainAdmission& a, const spx_ctx* ctx) {
 bool adm_acquire(spx_ctx* ctx) {
   const bool was = ctx->chain_denied;
   ctx->chain_denied = false;
+  // row shards own their GPUs and must all take the same chain: not admitted
+  // per process
+  if (ctx->sharded) return false;
   const int B = ctx->win_k ? chain_blocks(ctx, nullptr, true) : 0;
   if (B <= 0) return false;  // no persistent chain for this call anyway
   ChainAdmission& a = adm();
@@ -522,12 +549,20 @@ int enqueue_window_t(spx_ctx* ctx, int npiv, bool time_flush) {
   }
   if (B > 0) {
     const int cpb = (int)((ctx->N - 1 + B - 1) / B);  // (B * cpb == N-1: xown owns the RHS)
-    const int rpb = (int)((ctx->m_local + B - 1) / B);
-    auto kern = cb == 512 ? chain_kernel<KMAX, 512> : chain_kernel<KMAX, 256>;
+    const int rpb = (int)std::max<int64_t>(1, (ctx->m_local + B - 1) / B);
+    auto kern = ctx->sharded ? (cb == 512 ? chain_kernel<KMAX, 512, true>
+                                          : chain_kernel<KMAX, 256, true>)
+                             : (cb == 512 ? chain_kernel<KMAX, 512> : chain_kernel<KMAX, 256>);
+    ChainPeers pe = ctx->peers;
+    pe.stop_req = (const int32_t*)ctx->d_stop;
     hipLaunchKernelGGL(kern, dim3(B), dim3(cb), 0, ctx->stream, ctx->enter_part, ctx->st,
                        (const Params*)ctx->prm, std::max(NWAVE * ctx->nbn, B),
                        (const double*)ctx->A, ctx->ld, ctx->m_local, ctx->N, ctx->obj, ctx->win,
-                       npiv, ctx->basis, ctx->hist, ctx->gr_enter, ctx->gr_ratio, cpb, rpb);
+                       npiv, ctx->basis, ctx->hist, ctx->gr_enter, ctx->gr_ratio, cpb, rpb, pe);
+  } else if (ctx->sharded && !ctx->comm && !ctx->loop) {
+    ctx->err = "a peer-only shard needs the persistent chain (windowed, spx_peer_import done, "
+               "chain mode != 1, and its grid fits)";
+    return SPX_E_STATE;
   }
   for (int q = 0; B == 0 && q < npiv; ++q) {
     hipLaunchKernelGGL(lazy_ratio_kernel<KMAX>, dim3(nbw), dim3(BLK), 0, ctx->stream,
@@ -798,9 +833,21 @@ int alloc_common(spx_ctx* ctx, int64_t m_local, int64_t N, int64_t m_global, int
     HIPC(hipMemsetAsync(ctx->win.tag, 0, sizeof(uint32_t) * N, ctx->stream));
     HIPC(hipMemsetAsync(ctx->win.epoch, 0, sizeof(uint32_t), ctx->stream));
     const size_t ge = sizeof(unsigned long long) * ENTER_REC * CHAIN_MAX_BLOCKS;
-    const size_t gq = sizeof(unsigned long long) * RATIO_REC * CHAIN_MAX_BLOCKS;
+    // shards: every rank's records, two parity halves and the window-end plane
+    // (peers write them over xGMI: uncached, so this GPU's L2 never serves a
+    // stale copy to the local polls; plain memory between virtual ranks)
+    const size_t gq = sizeof(unsigned long long) *
+                      (ctx->sharded ? (size_t)CHAIN_SH_PLANES * CHAIN_SH_SLOTS
+                                    : (size_t)RATIO_REC * CHAIN_MAX_BLOCKS);
     HIPC(hipMalloc(&ctx->gr_enter, ge));
-    HIPC(hipMalloc(&ctx->gr_ratio, gq));
+    if (ctx->sharded && !ctx->loop) {
+      if (hipExtMallocWithFlags((void**)&ctx->gr_ratio, gq, hipDeviceMallocUncached) != hipSuccess) {
+        (void)hipGetLastError();
+        HIPC(hipMalloc(&ctx->gr_ratio, gq));
+      }
+    } else {
+      HIPC(hipMalloc(&ctx->gr_ratio, gq));
+    }
     HIPC(hipMemsetAsync(ctx->gr_enter, 0, ge, ctx->stream));
     HIPC(hipMemsetAsync(ctx->gr_ratio, 0, gq, ctx->stream));
   }
@@ -927,6 +974,148 @@ int spx_create_sharded_local(spx_ctx** out, int device, int rank, int nranks,
   G->members[rank] = ctx;
   G->refs++;
   ctx->loop = G;
+  return SPX_OK;
+}
+
+int spx_create_sharded_peer(spx_ctx** out, int device, int rank, int nranks) {
+  int rc = spx_create(out, device);
+  if (rc) return rc;
+  spx_ctx* ctx = *out;
+  CHECK_ARG(nranks >= 1 && nranks <= CHAIN_MAX_RANKS && rank >= 0 && rank < nranks,
+            "bad rank/nranks (peer shards: at most 16 ranks)");
+  ctx->rank = rank;
+  ctx->nranks = nranks;
+  ctx->sharded = true;
+  return SPX_OK;
+}
+
+// ---- the row-sharded persistent chain's peers ---------------
+namespace {
+struct PeerBlob {
+  uint32_t magic;
+  int32_t rank, nranks, device;
+  hipIpcMemHandle_t hA, hR;  // this rank's tableau and ratio-record buffer
+  int64_t ld, row0, m_local, N, m_global;
+  char bus[64];              // PCI bus id: which ranks share a GPU
+};
+constexpr uint32_t PEER_MAGIC = 0x53505850u;  // "SPXP"
+
+int peer_check(spx_ctx* ctx) {
+  CHECK_ARG(ctx->sharded && ctx->loaded, "peer chain: a loaded sharded context is needed");
+  CHECK_ARG(ctx->nranks <= CHAIN_MAX_RANKS, "peer chain: at most 16 ranks");
+  return SPX_OK;
+}
+}  // namespace
+
+int spx_peer_blob_size(void) { return (int)sizeof(PeerBlob); }
+
+// This rank's exchange blob (IPC handles of its tableau and record buffer,
+// its rows and GPU), to be all-gathered by the caller and given to
+// spx_peer_import on every rank.  Valid until the next load.
+int spx_peer_export(spx_ctx* ctx, void* out, int64_t cap) {
+  if (!ctx) return SPX_E_ARG;
+  int rc = peer_check(ctx);
+  if (rc) return rc;
+  CHECK_ARG(out && cap >= (int64_t)sizeof(PeerBlob), "blob buffer too small");
+  PeerBlob b;
+  std::memset(&b, 0, sizeof(b));
+  b.magic = PEER_MAGIC;
+  b.rank = ctx->rank;
+  b.nranks = ctx->nranks;
+  b.device = ctx->device;
+  HIPC(hipSetDevice(ctx->device));
+  HIPC(hipIpcGetMemHandle(&b.hA, ctx->A));
+  HIPC(hipIpcGetMemHandle(&b.hR, ctx->gr_ratio));
+  b.ld = ctx->ld;
+  b.row0 = ctx->row0;
+  b.m_local = ctx->m_local;
+  b.N = ctx->N;
+  b.m_global = ctx->m_global;
+  HIPC(hipDeviceGetPCIBusId(b.bus, (int)sizeof(b.bus) - 1, ctx->device));
+  std::memcpy(out, &b, sizeof(b));
+  return SPX_OK;
+}
+
+// Map every peer's tableau and record buffer (blobs: nranks blobs in rank
+// order, spx_peer_blob_size() bytes each).  Collective in effect: every rank
+// imports after every rank exported; afterwards windows of this context run
+// the row-sharded persistent chain when its grid fits.
+int spx_peer_import(spx_ctx* ctx, const void* blobs, int nranks) {
+  if (!ctx) return SPX_E_ARG;
+  int rc = peer_check(ctx);
+  if (rc) return rc;
+  CHECK_ARG(blobs && nranks == ctx->nranks, "peer import: one blob per rank");
+  close_peers(ctx);
+  HIPC(hipSetDevice(ctx->device));
+  const PeerBlob* bl = static_cast<const PeerBlob*>(blobs);
+  const PeerBlob& me = bl[ctx->rank];
+  ChainPeers pe{};
+  pe.rank = ctx->rank;
+  pe.nranks = nranks;
+  int same = 0;
+  for (int q = 0; q < nranks; ++q) {
+    const PeerBlob& b = bl[q];
+    CHECK_ARG(b.magic == PEER_MAGIC && b.rank == q && b.nranks == nranks && b.N == ctx->N &&
+                  b.m_global == ctx->m_global,
+              "peer import: blob mismatch (rank order, shape)");
+    same += std::strncmp(b.bus, me.bus, sizeof(b.bus)) == 0 ? 1 : 0;
+    pe.ld[q] = b.ld;
+    pe.row0[q] = b.row0;
+    if (q == ctx->rank) {
+      pe.A[q] = ctx->A;
+      pe.ratio[q] = ctx->gr_ratio;
+      continue;
+    }
+    void* pa = nullptr;
+    void* pr = nullptr;
+    hipError_t e = hipIpcOpenMemHandle(&pa, b.hA, hipIpcMemLazyEnablePeerAccess);
+    if (e == hipSuccess) ctx->ipc_open.push_back(pa);
+    if (e == hipSuccess) e = hipIpcOpenMemHandle(&pr, b.hR, hipIpcMemLazyEnablePeerAccess);
+    if (e == hipSuccess) ctx->ipc_open.push_back(pr);
+    if (e != hipSuccess) {
+      close_peers(ctx);
+      ctx->err = std::string("peer import: hipIpcOpenMemHandle: ") + hipGetErrorString(e);
+      return SPX_E_HIP;
+    }
+    pe.A[q] = static_cast<const double*>(pa);
+    pe.ratio[q] = static_cast<unsigned long long*>(pr);
+  }
+  ctx->peers = pe;
+  ctx->peer_same_dev = same;
+  ctx->peer_ok = true;
+  drop_graphs(ctx);
+  return SPX_OK;
+}
+
+// Virtual ranks (spx_create_sharded_local): the peers are this process's
+// group members.  Every rank calls it after its load (it meets the others).
+int spx_peer_chain_local(spx_ctx* ctx) {
+  if (!ctx) return SPX_E_ARG;
+  int rc = peer_check(ctx);
+  if (rc) return rc;
+  CHECK_ARG(ctx->loop != nullptr, "spx_peer_chain_local: not a virtual-rank context");
+  LoopGroup* G = ctx->loop;
+  if (!G->barrier()) return loop_fail(ctx);  // every member loaded
+  ChainPeers pe{};
+  pe.rank = ctx->rank;
+  pe.nranks = ctx->nranks;
+  int same = 0;
+  for (int q = 0; q < G->n; ++q) {
+    spx_ctx* m = G->members[q];
+    CHECK_ARG(m && m->loaded && m->N == ctx->N && m->m_global == ctx->m_global,
+              "spx_peer_chain_local: group member not loaded / shape mismatch");
+    pe.A[q] = m->A;
+    pe.ratio[q] = m->gr_ratio;
+    pe.ld[q] = m->ld;
+    pe.row0[q] = m->row0;
+    same += m->device == ctx->device ? 1 : 0;
+  }
+  if (!G->barrier()) return loop_fail(ctx);  // nobody reloads while the others read
+  close_peers(ctx);
+  ctx->peers = pe;
+  ctx->peer_same_dev = same;
+  ctx->peer_ok = true;
+  drop_graphs(ctx);
   return SPX_OK;
 }
 

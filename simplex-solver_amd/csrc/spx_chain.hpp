@@ -413,9 +413,20 @@ __device__ __forceinline__ void publish_record(Dst dst, int nd, int rs, unsigned
   }
 }
 
+// system-scope load of one double (the sharded chain's row gather from a peer)
+__device__ __forceinline__ double sys_load(const double* p) {
+  return __longlong_as_double((long long)__hip_atomic_load(
+      (gu64*)const_cast<double*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
+}
+
 // ---------------------------------------------------------------------------
-// chain_kernel<KMAX, CB>: the pivots of one window (npiv <= KMAX slots),
-// single GPU (row0 = 0).  grid = B blocks of CB threads (one block per CU,
+// chain_kernel<KMAX, CB, SH>: the pivots of one window (npiv <= KMAX slots).
+// SH = false: single GPU (row0 = 0).  SH = true: this rank's row block of a
+// row-sharded tableau: the columns, objective row and entering
+// exchange are replicated per rank (every rank computes the same values), the
+// ratio exchange is global (every block's record goes to every rank's
+// buffer, polled locally), and the leaving row's stale values are gathered
+// from the owner's tableau through a peer pointer.  grid = B blocks of CB threads (one block per CU,
 // every block resident); block b owns columns [b*cpb, ...) and rows
 // [b*rpb, ...), cpb, rpb <= CB, one of each per thread.  Wave 0 of a block
 // polls the record headers and hands the winner to the block through LDS;
@@ -425,12 +436,13 @@ __device__ __forceinline__ void publish_record(Dst dst, int nd, int rs, unsigned
 // previous window's chain); the chain writes one partial per block there for
 // the next window.
 // ---------------------------------------------------------------------------
-template <int KMAX, int CB>
+template <int KMAX, int CB, bool SH = false>
 __global__ __launch_bounds__(CB) void chain_kernel(
     Key* __restrict__ enter_part, State* st, const Params* __restrict__ prm, int n_ep,
     const double* __restrict__ A, int64_t ld, int64_t m, int64_t N, double* __restrict__ obj,
     Window win, int npiv, int64_t* __restrict__ basis, int64_t* __restrict__ hist,
-    unsigned long long* gr_enter_, unsigned long long* gr_ratio_, int cpb, int rpb) {
+    unsigned long long* gr_enter_, unsigned long long* gr_ratio_, int cpb, int rpb,
+    ChainPeers pe) {
   static_assert(KMAX <= 32, "slots are lane-indexed and fit the window buffers");
   constexpr int NW = CB / 64;
   constexpr int CH = KMAX % 8 == 0 ? 8 : KMAX % 4 == 0 ? 4 : 2;
@@ -474,7 +486,31 @@ __global__ __launch_bounds__(CB) void chain_kernel(
   const int64_t n_enter = prm->n_enter;
   const int64_t iter_limit = prm->iter_limit;
   const bool skip = prm->skip_zero != 0;
-  const uint32_t W = (E + 1u) & TAG_EPOCH;  // this window's epoch
+  const uint32_t W = (E + 1u) & TAG_EPOCH;  // this window's epoch (the same on every rank)
+  // row shards: my rank's rows start at row0; the ratio records of all nr * B
+  // blocks are polled (block slot rank * B + b, planes RS apart)
+  const int rank = SH ? pe.rank : 0;
+  const int nr = SH ? pe.nranks : 1;
+  const int64_t row0 = SH ? pe.row0[rank] : 0;
+  constexpr int RS = SH ? CHAIN_SH_SLOTS : CHAIN_MAX_BLOCKS;
+  const int BR = SH ? nr * B : B;
+  const int bs = SH ? rank * B + b : b;
+  // rank 0's time-limit stop request rides in its ratio records (bit 31 of
+  // granule 3); read once per window, so every rank stops at the window's start
+  const unsigned stopbit =
+      (SH && rank == 0 && pe.stop_req &&
+       __hip_atomic_load(const_cast<int32_t*>(pe.stop_req), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_SYSTEM) != 0)
+          ? 1u : 0u;
+  // the ratio buffer of pivot it0 + q: SH alternates two halves by pivot
+  // parity (a rank's entering exchange is local, so it may publish ratio
+  // q + 1 before a peer has read ratio q; never q + 2)
+  auto ratio_buf = [&](int d, int qq) -> gu64* {
+    if constexpr (SH)
+      return (gu64*)pe.ratio[d] + (size_t)((it0 + qq) & 1) * RATIO_REC * RS;
+    else
+      return gr_ratio;
+  };
   // my column and my row
   const int64_t j = (int64_t)b * cpb + t;
   const bool jlive = t < cpb && j < N;
@@ -483,9 +519,10 @@ __global__ __launch_bounds__(CB) void chain_kernel(
   // issues no row-side stores (f_q) that its next poll's vmcnt wait would
   // also have to drain; the pivot bookkeeping is stored by the last thread
   const int roff = rpb <= CB - 64 ? 64 : 0;
-  const int64_t i = (int64_t)b * rpb + (t - roff);
+  const int64_t i = (int64_t)b * rpb + (t - roff);  // local row
   const bool ilive = t >= roff && t - roff < rpb && i < m;
   const int64_t ic = ilive ? i : 0;
+  const int64_t ig = row0 + i;  // global row (what records, slots and basis speak)
   double o = obj[jc];
   uint32_t tg = jlive ? win.tag[jc] : 0u;
   const uint32_t tg0 = tg;
@@ -501,7 +538,7 @@ __global__ __launch_bounds__(CB) void chain_kernel(
   uint32_t zmx = 0u;
   __shared__ double pxl[KMAX];  // p_s[N-1] (xown only)
   double bcur = A[(N - 1) * ld + ic];   // current RHS of my row (stale + applied slots)
-  int64_t bas = basis[ic];              // basis[i] (Bland's tie key)
+  int64_t bas = basis[row0 + ic];       // basis[ig] (Bland's tie key)
   double fs[KMAX], ps[KMAX];            // f_s[i], p_s[j] of this window
 #pragma unroll
   for (int s = 0; s < KMAX; ++s) fs[s] = ps[s] = 0.0;
@@ -544,7 +581,8 @@ __global__ __launch_bounds__(CB) void chain_kernel(
       if (w0) {
         KeyP e;
         const bool ok =
-            poll_records<false, 3>(gr_enter, B, rec_tag(W, q - 1, GK_ENTER), rule, e, st);
+            poll_records<false, 3>(gr_enter, B, CHAIN_MAX_BLOCKS, rec_tag(W, q - 1, GK_ENTER),
+                                   rule, e, st);
         if (t == 0) {
           bc_idx = ok ? e.row : -2;
           bc_val = e.a;
@@ -576,12 +614,12 @@ __global__ __launch_bounds__(CB) void chain_kernel(
     }
     double pcl = 0.0, unused[2];
     if (q > 0 &&
-        !load_extras<0>(gr_enter, wb, ENTER_HDR, q, 0, rec_tag(W, q - 1, GK_ENTER), pcl, unused,
-                        st))
+        !load_extras<0>(gr_enter, CHAIN_MAX_BLOCKS, wb, ENTER_HDR, q, 0,
+                        rec_tag(W, q - 1, GK_ENTER), pcl, unused, st))
       return;
     SPX_PROBE(q, 2, 0, fv != 12345.678 && pcl != 12345.678);  // loads arrived
     // RHS: apply slot q-1 (the slots before it are already in bcur)
-    if (q > 0) bcur = apply_sel(bcur, i == r_prev, false, true, f_prev, prhs, skip);
+    if (q > 0) bcur = apply_sel(bcur, ig == r_prev, false, true, f_prev, prhs, skip);
     // apply_sel's special cases as masks: column c entered earlier in this
     // window or p_s[c] == 0 under the skip rule (uniform: the exact loop), my
     // row left at slot s (rmask: p_s[c] replaces the msub on that lane).
@@ -623,7 +661,7 @@ __global__ __launch_bounds__(CB) void chain_kernel(
           for (int u = 0; u < CH; ++u) {
             const int s = c8 + u;
             const bool act = s < q;
-            const bool isr = i == rdlane64(slot_r, s);
+            const bool isr = ig == rdlane64(slot_r, s);
             const bool isc = c == rdlane64(slot_c, s);
             fv = apply_sel(fv, isr, isc, act, fs[s], rdlane(pcl, s), skip);
           }
@@ -641,17 +679,17 @@ __global__ __launch_bounds__(CB) void chain_kernel(
     KeyP k = keyp_none();
     if (ilive) {
       if (forced_r >= 0) {
-        if (i == forced_r) kmin2(k, 0.0, 0, i, 0.0, 0.0);
+        if (ig == forced_r) kmin2(k, 0.0, 0, ig, 0.0, 0.0);
       } else if (fv > eps_piv) {
         const double rq = bcur / fv;
-        if (rq == rq) kmin2(k, rq, rule == RULE_BLAND ? bas : i, i, 0.0, 0.0);
+        if (rq == rq) kmin2(k, rq, rule == RULE_BLAND ? bas : ig, ig, 0.0, 0.0);
       }
     }
     SPX_PROBE(q, 0, 2, fv != 12345.678);
     // publish: the wave winner puts its f history and RHS in LDS, the block's
     // winner is published by wave 0 (rows grow with the lane: Dantzig's tie key)
     k = key_of_lane(k, wave_argmin(k.v, k.t, k.row >= 0, rule != RULE_BLAND));
-    if (ilive && k.row == i) {
+    if (ilive && k.row == ig) {
       if constexpr (LH) {
         hl33[w] = bcur;
       } else {
@@ -666,14 +704,17 @@ __global__ __launch_bounds__(CB) void chain_kernel(
     __syncthreads();
     SPX_PROBE(q, 2, 3, true);              // every wave of the block arrived
     if (w0) {
-      publish_record<NW, true>(gr_ratio, b, rec_tag(W, q, GK_RATIO), q + 1, sk,
-                               [&](int ww, int64_t row, int x) -> double {
-                                 if constexpr (LH)
-                                   return x == 33 ? hl33[ww]
-                                                  : fsl[x][(int)(row - (int64_t)b * rpb) + roff];
-                                 else
-                                   return hl[ww][x];
-                               });
+      publish_record<NW, true, SH>([&](int d) { return ratio_buf(d, q) + bs; }, nr, RS,
+                                   rec_tag(W, q, GK_RATIO), q + 1, sk,
+                                   [&](int ww, int64_t row, int x) -> double {
+                                     if constexpr (LH)
+                                       return x == 33 ? hl33[ww]
+                                                      : fsl[x][(int)(row - row0 - (int64_t)b * rpb) +
+                                                               roff];
+                                     else
+                                       return hl[ww][x];
+                                   },
+                                   stopbit);
       SPX_PROBE_CHAIN(q, 0);
     }
     // f_q for the flush / row_fix (later kernels): stored after the record, so
@@ -685,11 +726,13 @@ __global__ __launch_bounds__(CB) void chain_kernel(
     if (w0) {
       KeyP rk;
       const unsigned rtag = rec_tag(W, q, GK_RATIO);
-      const bool ok = rule == RULE_BLAND
-                          ? poll_records<true, 4>(gr_ratio, B, rtag, rule, rk, st)
-                          : poll_records<true, 3>(gr_ratio, B, rtag, rule, rk, st);
+      bool stopq = false;
+      const bool ok =
+          SH ? poll_records<true, 4, true>(ratio_buf(rank, q), BR, RS, rtag, rule, rk, st, &stopq)
+          : rule == RULE_BLAND ? poll_records<true, 4>(gr_ratio, B, RS, rtag, rule, rk, st)
+                               : poll_records<true, 3>(gr_ratio, B, RS, rtag, rule, rk, st);
       if (t == 0) {
-        bc_idx = ok ? rk.row : -2;
+        bc_idx = ok ? (stopq ? -3 : rk.row) : -2;
         bc_blk = (int)rk.b;
       }
       SPX_PROBE_CHAIN(q, 1);
@@ -700,20 +743,31 @@ __global__ __launch_bounds__(CB) void chain_kernel(
     if (r == -2) return;
     SPX_PROBE(q, 1, 1, true);
     if (q == 0 && leader) *win.epoch = W;  // every block has read E (its record carries W)
+    if (r == -3) {  // (SH) rank 0's time-limit stop, seen by every rank at this pivot
+      stop_status = ST_LIMIT;
+      break;
+    }
     if (r < 0) {
       stop_status = ST_UNBOUNDED;
       break;
     }
     // row r on my column: stale + pending slots.  f_s[r] (lane s <= q, lane q
     // the pivot element) and the row's RHS from the winning ratio record
-    double v = A[jc * ld + r];
+    double v;
+    if constexpr (SH) {  // the owner's stale row (a peer's tableau unless it is mine)
+      const int own = wb / B;
+      if (own == rank) v = A[jc * ld + (r - row0)];
+      else v = sys_load(pe.A[own] + jc * pe.ld[own] + (r - pe.row0[own]));
+    } else {
+      v = A[jc * ld + r];
+    }
     if constexpr (LH) {  // my column's p history, read while the gathers are in flight
 #pragma unroll
       for (int s = 0; s < KMAX; ++s) ps[s] = psl[s][t];
     }
     double frl = 0.0, ex[2];
-    if (!load_extras<1>(gr_ratio, wb, RATIO_HDR + 2, q + 1, RATIO_HDR, rec_tag(W, q, GK_RATIO),
-                        frl, ex, st))
+    if (!load_extras<1, SH>(ratio_buf(rank, q), RS, wb, RATIO_HDR + 2, q + 1, RATIO_HDR,
+                            rec_tag(W, q, GK_RATIO), frl, ex, st))
       return;
     SPX_PROBE(q, 3, 0, v != 12345.678 && frl != 12345.678);  // loads arrived
     const double piv = rdlane(frl, q);
@@ -807,8 +861,8 @@ __global__ __launch_bounds__(CB) void chain_kernel(
       }
       pxl[q] = prhs;
     }
-    if (ilive && i == r) bas = c;
-    rmask |= (i == r) ? (1u << q) : 0u;
+    if (ilive && ig == r) bas = c;
+    rmask |= (ig == r) ? (1u << q) : 0u;
     if (lane == q) {
       slot_r = r;
       slot_c = c;
@@ -829,7 +883,8 @@ __global__ __launch_bounds__(CB) void chain_kernel(
     SPX_PROBE(q, 3, 3, true);               // every wave of the block arrived
     if (w0) {
       if (q + 1 < npiv) {
-        publish_record<NW, false>(gr_enter, b, rec_tag(W, q, GK_ENTER), q + 1, sk,
+        publish_record<NW, false>([&](int) { return gr_enter + b; }, 1, CHAIN_MAX_BLOCKS,
+                                  rec_tag(W, q, GK_ENTER), q + 1, sk,
                                   [&](int ww, int64_t col, int x) -> double {
                                     if constexpr (LH)
                                       return psl[x][(int)(col - (int64_t)b * cpb)];
@@ -867,6 +922,27 @@ __global__ __launch_bounds__(CB) void chain_kernel(
     }
 
     SPX_PROBE(q, 1, 3, true);
+  }
+  if constexpr (SH) {
+    // Window-end barrier: a rank's next kernels (flush, row_fix) rewrite its
+    // rows, so none may start while a peer still gathers one of them.  Every
+    // block reports once its last row gather has returned (its values were
+    // consumed before the last block barrier above); block 0 of every rank
+    // waits for all nr * B reports, so no rank's chain launch completes
+    // before every rank is done reading.
+    if (w0) {
+      const unsigned dtag = rec_tag(W, 0, GK_DONE);
+      if (lane < nr)
+        g_store<true>((gu64*)pe.ratio[lane] + (size_t)2 * RATIO_REC * RS + bs, dtag, 0u);
+      if (b == 0) {
+        const gu64* dp = (const gu64*)pe.ratio[rank] + (size_t)2 * RATIO_REC * RS;
+        for (unsigned spins = 0;;) {
+          bool ok = true;
+          for (int x = lane; x < BR; x += 64) ok &= (unsigned)(g_load<true>(dp + x) >> 32) == dtag;
+          if (__all(ok) || spin_fail(spins, st)) break;
+        }
+      }
+    }
   }
   // ---- the window ends after slot q (q pivots made) ----
   if (stop_status != ST_RUNNING && leader) {

@@ -104,6 +104,12 @@ SIGNATURES = {
                                         ctypes.POINTER(ctypes.c_int64), ctypes.c_int]),
     "spx_get_chain": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_int)]),
     "spx_set_chain_budget": (ctypes.c_int, [ctypes.c_int, ctypes.c_int]),
+    "spx_create_sharded_peer": (ctypes.c_int, [ctypes.POINTER(_P), ctypes.c_int, ctypes.c_int,
+                                               ctypes.c_int]),
+    "spx_peer_blob_size": (ctypes.c_int, []),
+    "spx_peer_export": (ctypes.c_int, [_P, ctypes.c_void_p, _I64]),
+    "spx_peer_import": (ctypes.c_int, [_P, ctypes.c_char_p, ctypes.c_int]),
+    "spx_peer_chain_local": (ctypes.c_int, [_P]),
     "spx_get_chain_stats": (ctypes.c_int, [_P, _LP]),
     "spx_get_elim_variant": (ctypes.c_int, [_P, _LP]),
     "spx_get_flush_variant": (ctypes.c_int, [_P, _LP]),

@@ -55,11 +55,40 @@ def exchange_unique_id(make_id=make_unique_id, group=None) -> bytes:
 class ShardedTableau(DeviceTableau):
     """This rank's row block of a tableau sharded over `world` GPUs."""
 
-    def __init__(self, device: int, rank: int, world: int, uid: bytes, local: bool = False):
+    def __init__(self, device: int, rank: int, world: int, uid: bytes | None = None,
+                 local: bool | str = False):
         """local=True: the ranks are threads of this process sharing GPUs
-        (in-process loopback exchange instead of RCCL; for tests)."""
+        (in-process loopback exchange instead of RCCL; for tests).
+        local="peer": no communicator at all; the ranks exchange only through
+        the row-sharded persistent chain (enable_peer_chain is then required)."""
         super().__init__(device, _sharded=(rank, world, uid, local))
-        self.rank, self.world = rank, world
+        self.rank, self.world, self.local = rank, world, local
+
+    def enable_peer_chain(self, allgather=None) -> None:
+        """Set up the row-sharded persistent chain for the loaded rows (DESIGN.md
+        §5): every rank calls this after its load.  Virtual ranks meet in
+        process; otherwise this rank's blob (IPC handles of its tableau and
+        record buffer) is all-gathered with `allgather(bytes) -> list[bytes]`
+        (default: torch.distributed.all_gather_object) and imported."""
+        lib = self._lib
+        if self.local is True:
+            self._check(lib.spx_peer_chain_local(self._ctx), "spx_peer_chain_local")
+            return
+        size = lib.spx_peer_blob_size()
+        buf = ctypes.create_string_buffer(size)
+        self._check(lib.spx_peer_export(self._ctx, buf, size), "spx_peer_export")
+        if allgather is None:
+            import torch.distributed as tdist
+
+            def allgather(blob):
+                out = [None] * tdist.get_world_size()
+                tdist.all_gather_object(out, blob)
+                return out
+        blobs = allgather(buf.raw)
+        if len(blobs) != self.world or any(len(b) != size for b in blobs):
+            raise RuntimeError("peer chain: bad blob exchange")
+        self._check(lib.spx_peer_import(self._ctx, b"".join(blobs), self.world),
+                    "spx_peer_import")
 
     @classmethod
     def from_env(cls, device: int | None = None, group=None) -> "ShardedTableau":

@@ -93,8 +93,13 @@ class DeviceTableau:
             rc = self._lib.spx_create(ctypes.byref(self._ctx), int(device))
         else:
             rank, nranks, uid, local = _sharded
-            create = self._lib.spx_create_sharded_local if local else self._lib.spx_create_sharded
-            rc = create(ctypes.byref(self._ctx), int(device), int(rank), int(nranks), uid)
+            if local == "peer":  # no communicator: the persistent chain's peers only
+                rc = self._lib.spx_create_sharded_peer(ctypes.byref(self._ctx), int(device),
+                                                       int(rank), int(nranks))
+            else:
+                create = (self._lib.spx_create_sharded_local if local
+                          else self._lib.spx_create_sharded)
+                rc = create(ctypes.byref(self._ctx), int(device), int(rank), int(nranks), uid)
         if rc != 0:
             msg = self._err()
             self.close()

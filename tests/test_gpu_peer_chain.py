@@ -1,0 +1,190 @@
+"""The row-sharded persistent chain (chain_kernel<.., SH = true>).
+
+Each rank runs ONE persistent launch per window over its row block; the ratio
+records of every rank's blocks are written to every rank's record buffer, and
+the leaving row is gathered from its owner's tableau through a peer pointer.
+Bar: every rank's rows, the replicated objective row and basis, the pivot
+sequence and the status equal the CPU oracle's (bit-exact), and equal the
+launch-per-phase sharded path's.
+
+Peers are exercised two ways on one GPU: virtual ranks (threads of this
+process, plain device pointers) and two processes exchanging IPC handles over
+gloo (spx_create_sharded_peer: no RCCL, which refuses two ranks on one GPU).
+"""
+import os
+import socket
+import subprocess
+import sys
+import threading
+
+import numpy as np
+import pytest
+
+from oracle import simplex_oracle as O
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _peer_threads(world, kind, m, n, seed, rule, K, peer=True, mode=0, **solve_kw):
+    """world virtual ranks on GPU 0, each loading its rows and (peer=True)
+    joining the row-sharded persistent chain; returns rank -> results."""
+    from simplex_amd import dist, synth
+    uid = bytes([world, m % 251, n % 251, seed % 251, 7]) + os.urandom(123)
+    outs, errors = {}, []
+
+    def rank_main(rank):
+        try:
+            r0, r1 = dist.row_partition(m, world, rank)
+            T, obj, basis = synth.tableau_rows(kind, m, n, seed, r0, r1, order="F")
+            with dist.ShardedTableau(0, rank, world, uid, local=True) as s:
+                s.set_window(K)
+                s.set_chain(mode)
+                s.load_shard(T, obj, basis, m, r0)
+                if peer:
+                    s.enable_peer_chain()
+                blocks = s.chain_blocks()
+                res = s.solve(rule=rule, **solve_kw)
+                outs[rank] = (r0, r1, res, s.history().tolist(), s.tableau(), s.basis(), blocks)
+        except Exception as ex:  # pragma: no cover
+            errors.append(ex)
+
+    th = [threading.Thread(target=rank_main, args=(r,)) for r in range(world)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=600)
+    assert not errors, errors
+    return outs
+
+
+def _check_vs_oracle(outs, kind, m, n, seed, rule, max_iters=200000):
+    from simplex_amd import synth
+    T, basis = synth.full_tableau(kind, m, n, seed)
+    st, hist = O.solve_tableau(T, basis, rule=rule, max_iters=max_iters)
+    for rank, (r0, r1, res, h, Tl, b, blocks) in outs.items():
+        assert res.status == st
+        assert [tuple(x) for x in h] == hist
+        assert np.array_equal(Tl[:-1], T[r0:r1])
+        assert np.array_equal(Tl[-1], T[-1])
+        assert np.array_equal(b, basis)
+    return st, hist
+
+
+@pytest.mark.parametrize("world,kind,m,n,rule,K", [
+    (1, "dense", 200, 300, "dantzig", 8),
+    (2, "dense", 200, 300, "dantzig", 8),
+    (3, "dense", 301, 257, "dantzig", 24),
+    (4, "dense", 1024, 2048, "dantzig", 16),
+    (2, "degenerate", 64, 64, "bland", 12),
+    (3, "degenerate", 96, 96, "bland", 32),
+    (5, "dense", 7, 9, "dantzig", 4),   # ranks with one or two rows
+])
+def test_peer_chain_virtual_ranks_bit_exact(world, kind, m, n, rule, K):
+    outs = _peer_threads(world, kind, m, n, 3, rule, K)
+    assert all(o[6] >= 1 for o in outs.values()), "the persistent sharded chain did not run"
+    _check_vs_oracle(outs, kind, m, n, 3, rule)
+
+
+@pytest.mark.parametrize("world,K", [(2, 24), (3, 24), (2, 32)])
+def test_peer_chain_config3_width(world, K):
+    """Config-3 width (N - 1 = 16384 candidate columns: 64 blocks per rank,
+    the RHS column riding along), 2-3 ranks' chains resident on one GPU,
+    partial last window; the same bytes as the launch-per-phase sharded path."""
+    kw = dict(max_iters=5 * K + 7)
+    m, n = 400, 15984
+    outs = _peer_threads(world, "dense", m, n, 9, "dantzig", K, **kw)
+    assert all(o[6] == 64 for o in outs.values())
+    lazy = _peer_threads(world, "dense", m, n, 9, "dantzig", K, peer=False, **kw)
+    for r in range(world):
+        assert outs[r][3] == lazy[r][3] and outs[r][4].tobytes() == lazy[r][4].tobytes()
+    _check_vs_oracle(outs, "dense", m, n, 9, "dantzig", max_iters=5 * K + 7)
+
+
+def test_peer_chain_mode1_falls_back_to_lazy():
+    """chain mode 1 on every rank: the launch-per-phase sharded path runs
+    (chain_blocks 0) with the same result."""
+    outs = _peer_threads(2, "dense", 200, 300, 4, "dantzig", 8, mode=1)
+    assert all(o[6] == 0 for o in outs.values())
+    _check_vs_oracle(outs, "dense", 200, 300, 4, "dantzig")
+
+
+def test_peer_chain_time_limit_stops_every_rank_together():
+    """rank 0's stop request rides in its ratio records: every rank stops at
+    the same window start with status 1."""
+    m, n, K = 600, 900, 8
+    outs = _peer_threads(3, "dense", m, n, 5, "dantzig", K, time_limit=1e-4)
+    iters = {o[2].iters for o in outs.values()}
+    assert len(iters) == 1
+    k = iters.pop()
+    assert k % K == 0 and all(o[2].status == 1 for o in outs.values())
+    _check_vs_oracle(outs | {}, "dense", m, n, 5, "dantzig", max_iters=k)
+
+
+def test_peer_chain_resume_and_forced_pivots():
+    """Several calls per context (limits mid-window), then a forced pivot
+    (spx_pivot_at) on a row owned by rank 1, then a full solve."""
+    from simplex_amd import dist, synth
+    m, n, world = 120, 200, 2
+    uid = b"peer-resume" + os.urandom(117)
+    outs, errors = {}, []
+    # the forced pivot: a nonbasic column with a solid entry in row 90 after 16 pivots
+    T, basis = synth.full_tableau("dense", m, n, 6)
+    _, h1 = O.solve_tableau(T, basis, max_iters=16)
+    fc = next(j for j in range(n + m) if j not in set(basis.tolist()) and abs(T[90, j]) > 0.05)
+
+    def rank_main(rank):
+        try:
+            r0, r1 = dist.row_partition(m, world, rank)
+            T, obj, basis = synth.tableau_rows("dense", m, n, 6, r0, r1, order="F")
+            with dist.ShardedTableau(0, rank, world, uid, local=True) as s:
+                s.set_window(8)
+                s.load_shard(T, obj, basis, m, r0)
+                s.enable_peer_chain()
+                s.solve(max_iters=5)
+                s.solve(max_iters=11)
+                s.pivot_at(90, fc)
+                s.solve(max_iters=60)
+                outs[rank] = (r0, r1, s.history().tolist(), s.tableau(), s.basis())
+        except Exception as ex:  # pragma: no cover
+            errors.append(ex)
+
+    th = [threading.Thread(target=rank_main, args=(r,)) for r in range(world)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=300)
+    assert not errors, errors
+    O.pivot(T, 90, fc)
+    basis[90] = fc
+    _, h2 = O.solve_tableau(T, basis, max_iters=60)
+    for rank, (r0, r1, h, Tl, b) in outs.items():
+        assert [tuple(x) for x in h] == h1 + [(90, fc)] + h2
+        assert np.array_equal(Tl[:-1], T[r0:r1]) and np.array_equal(Tl[-1], T[-1])
+        assert np.array_equal(b, basis)
+
+
+def _free_port():
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("args", [
+    ["--m", "600", "--n", "900", "--window", "8"],
+    ["--m", "400", "--n", "15984", "--window", "24", "--pivots", "100"],
+])
+def test_peer_chain_two_processes_ipc(args):
+    """Two processes on GPU 0, no RCCL: IPC handles of each rank's tableau and
+    record buffer exchanged over gloo (spx_peer_export / spx_peer_import), the
+    persistent chains of both processes resident together; rank 0 checks every
+    rank bit-exactly against the oracle (tools/rccl_ranks_check.py --peer 2)."""
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", HSA_ENABLE_IPC_MODE_LEGACY="0")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.join(ROOT, "tools", "rccl_ranks_check.py"), "--peer", "2", "--same-device",
+           *args]
+    p = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=280)
+    out = p.stdout + p.stderr
+    assert p.returncode == 0 and "RCCL_RANKS_CHECK PASS" in out, out[-4000:]

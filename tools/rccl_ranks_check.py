@@ -1,11 +1,17 @@
-"""Multi-process RCCL check of the row-sharded pivot path.
+"""Multi-process check of the row-sharded pivot path.
 
 Launch: python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 \\
-        tools/rccl_ranks_check.py [--m M --n N --pivots K --same-device]
-Every rank loads its row block, runs the pivots through libspx's RCCL
-all-gather, and rank 0 checks every rank's rows, the objective row and the
-pivot sequence against the CPU oracle (bit-exact).  --same-device puts all ranks
-on GPU 0 (only if the RCCL build allows several ranks per device).
+        tools/rccl_ranks_check.py [--m M --n N --pivots K --window K --peer P --same-device]
+Every rank loads its row block and runs the pivots, then rank 0 checks every
+rank's rows, the objective row and the pivot sequence against the CPU oracle
+(bit-exact) and exits non-zero on a mismatch.
+
+  --peer 0  RCCL all-gather per pivot (launch-per-phase windows, or single pivots)
+  --peer 1  RCCL context + the row-sharded persistent chain (IPC-mapped peers)
+  --peer 2  no communicator at all: the persistent chain's peers only
+            (spx_create_sharded_peer; works with several ranks on one GPU,
+            which RCCL refuses)
+--same-device puts all ranks on GPU 0.
 """
 import argparse
 import os
@@ -24,34 +30,54 @@ def main():
     ap.add_argument("--m", type=int, default=300)
     ap.add_argument("--n", type=int, default=500)
     ap.add_argument("--pivots", type=int, default=0)
+    ap.add_argument("--window", type=int, default=0)
+    ap.add_argument("--peer", type=int, default=0, choices=[0, 1, 2])
+    ap.add_argument("--rule", default="dantzig")
+    ap.add_argument("--kind", default="dense")
+    ap.add_argument("--seed", type=int, default=17)
     ap.add_argument("--same-device", action="store_true")
     a = ap.parse_args()
     dist.init_process_group("gloo")
     rank, world = dist.get_rank(), dist.get_world_size()
     local = int(os.environ.get("LOCAL_RANK", rank))
     from simplex_amd import dist as sdist, synth
-    uid = sdist.exchange_unique_id()
     dev = 0 if a.same_device else local
     r0, r1 = sdist.row_partition(a.m, world, rank)
-    T, obj, basis = synth.tableau_rows("dense", a.m, a.n, 17, r0, r1, order="F")
-    with sdist.ShardedTableau(dev, rank, world, uid) as s:
+    T, obj, basis = synth.tableau_rows(a.kind, a.m, a.n, a.seed, r0, r1, order="F")
+    if a.peer == 2:
+        s = sdist.ShardedTableau(dev, rank, world, local="peer")
+    else:
+        s = sdist.ShardedTableau(dev, rank, world, sdist.exchange_unique_id())
+    with s:
+        s.set_window(a.window)
         s.load_shard(T, obj, basis, a.m, r0)
-        res = s.solve(max_iters=a.pivots, use_graph=True)
-        out = (r0, r1, res.status, s.history().tolist(), s.tableau(), s.basis())
+        if a.peer:
+            s.enable_peer_chain()
+        blocks = s.chain_blocks()
+        res = s.solve(max_iters=a.pivots, rule=a.rule, use_graph=True)
+        out = (r0, r1, res.status, s.history().tolist(), s.tableau(), s.basis(), blocks)
     outs = [None] * world
     dist.all_gather_object(outs, out)
+    ok = True
     if rank == 0:
         from oracle import simplex_oracle as O
-        Tf, bf = synth.full_tableau("dense", a.m, a.n, 17)
-        st, hist = O.solve_tableau(Tf, bf, max_iters=a.pivots)
-        ok = True
-        for q, (r0, r1, stq, h, Tl, b) in enumerate(outs):
+        Tf, bf = synth.full_tableau(a.kind, a.m, a.n, a.seed)
+        st, hist = O.solve_tableau(Tf, bf, rule=a.rule, max_iters=a.pivots)
+        for q, (r0, r1, stq, h, Tl, b, nb) in enumerate(outs):
             good = ([tuple(x) for x in h] == hist and np.array_equal(Tl[:-1], Tf[r0:r1])
-                    and np.array_equal(Tl[-1], Tf[-1]) and np.array_equal(b, bf))
-            print(f"rank {q}: rows {r0}:{r1} status {stq} pivots {len(h)} bit-exact {good}")
+                    and np.array_equal(Tl[-1], Tf[-1]) and np.array_equal(b, bf)
+                    and stq == st)
+            print(f"rank {q}: rows {r0}:{r1} status {stq} pivots {len(h)} chain blocks {nb} "
+                  f"bit-exact {good}", flush=True)
             ok &= good
-        print("RCCL_RANKS_CHECK", "PASS" if ok else "FAIL", f"world={world} pivots={len(hist)}")
+        if a.peer:
+            ok &= all(o[6] > 0 for o in outs)  # the persistent chain ran
+        print("RCCL_RANKS_CHECK", "PASS" if ok else "FAIL",
+              f"world={world} peer={a.peer} window={a.window} pivots={len(hist)}", flush=True)
+    flag = [ok]
+    dist.broadcast_object_list(flag, src=0)
     dist.destroy_process_group()
+    sys.exit(0 if flag[0] else 1)
 
 
 if __name__ == "__main__":
