@@ -68,6 +68,10 @@ def parse():
                          "single GPU), 1 two launches per pivot, 2 / 3 persistent with 256- / "
                          "512-thread blocks")
     ap.add_argument("--chain-blocks", type=int, default=0, help="persistent chain grid (0: minimum)")
+    ap.add_argument("--peer", type=int, default=1,
+                    help="N > 1 windows: 1 the row-sharded persistent chain (peer records over "
+                         "xGMI, after a bit-exact self-test against the RCCL path), 0 one RCCL "
+                         "all-gather per pivot")
     ap.add_argument("--time-every", type=int, default=0,
                     help="HIP events around every k-th elimination (or window flush) of the "
                          "timed region (0: 8 eliminations / 4 flushes; an event node costs "
@@ -89,32 +93,45 @@ def dist_env():
 def cpu_baseline(m, n, seed, rule, budget_s, gpu_hist):
     """Time the CPU oracle on the same config-3 tableau (rank 0, N=1 only).
 
-    Primary figure: the C/OpenMP restatement (oracle/spx_oracle.c) on all the
-    host threads OpenMP is allowed (OMP_NUM_THREADS).  Also reported: the numpy
-    oracle, 1 thread.  Both must reproduce the GPU's first pivots exactly."""
+    Primary figure: the C/OpenMP restatement (oracle/spx_oracle.c: p[j] == 0
+    columns neither read nor written, touched columns as vectorised runs, rows
+    over threads) with as many threads as this job's CPU share allows
+    (OMP_NUM_THREADS, 16 per GPU on the box; the box's other cores belong to
+    other jobs).  Also reported: the same C code on 1 thread and the numpy
+    oracle (1 thread).  All must reproduce the GPU's first pivots exactly."""
     from oracle import c_oracle as C
     from oracle import simplex_oracle as O
     from simplex_amd import synth
     Tf, obj, basis0 = synth.tableau_rows("dense", m, n, seed, order="C")
     T = np.vstack([Tf, obj[None, :]])
     del Tf
-    out = {}
-    # C / OpenMP
-    Tc, bc = T.copy(), basis0.copy()
-    k, hist, t0 = 0, [], time.perf_counter()
-    while time.perf_counter() - t0 < budget_s and k < 5000:
-        st, h = C.solve(Tc, bc, rule=rule, max_iters=1, hist_cap=1)
-        if st != 1:  # no pivot made (optimal / unbounded)
-            break
-        hist += h
-        k += 1
-    el = time.perf_counter() - t0
+
+    def c_run(threads, secs, Tc, bc, hist):
+        C.set_threads(threads)
+        k, t0 = 0, time.perf_counter()
+        while time.perf_counter() - t0 < secs and k < 5000:
+            st, h = C.solve(Tc, bc, rule=rule, max_iters=1, hist_cap=1)
+            if st != 1:  # no pivot made (optimal / unbounded)
+                break
+            hist += h
+            k += 1
+        return k, time.perf_counter() - t0
+
+    def matches(h):
+        kk = min(len(h), len(gpu_hist))
+        return [tuple(x) for x in gpu_hist[:kk]] == h[:kk]
+
+    threads = C.threads()  # OMP_NUM_THREADS
+    Tc, bc, hist = T.copy(), basis0.copy(), []
+    k, el = c_run(threads, budget_s * 0.6, Tc, bc, hist)
+    # 1 thread, continuing the same sequence
+    k1, el1 = c_run(1, budget_s * 0.2, Tc, bc, hist)
+    C.set_threads(threads)
     del Tc
-    kk = min(k, len(gpu_hist))
-    out["c"] = (k, el, [tuple(x) for x in gpu_hist[:kk]] == hist[:kk])
+    ok = matches(hist)
     # numpy, 1 thread
     k2, hist2, t0 = 0, [], time.perf_counter()
-    while time.perf_counter() - t0 < budget_s / 3 and k2 < 2000:
+    while time.perf_counter() - t0 < budget_s * 0.2 and k2 < 2000:
         c = O.select_entering(T[-1], T.shape[1] - 1, rule, 1e-9)
         r = O.ratio_test(T, c, basis0, rule, 1e-12)
         O.pivot(T, r, c)
@@ -122,30 +139,87 @@ def cpu_baseline(m, n, seed, rule, budget_s, gpu_hist):
         hist2.append((r, c))
         k2 += 1
     el2 = time.perf_counter() - t0
-    kk = min(k2, len(gpu_hist))
-    out["np"] = (k2, el2, [tuple(x) for x in gpu_hist[:kk]] == hist2[:kk])
-    k, el, ok = out["c"]
-    k2, el2, ok2 = out["np"]
-    return {"value": k / el, "unit": "pivots/s", "cores": C.threads(), "kind": "port",
+    ok2 = matches(hist2)
+    return {"value": k / el, "unit": "pivots/s", "cores": threads, "kind": "port",
             "sample": f"C/OpenMP oracle (oracle/spx_oracle.c), first {k} {rule} pivots of the "
-                      f"same {m}x{n} tableau from the slack basis, {el:.1f} s, "
-                      f"{C.threads()} threads",
+                      f"same {m}x{n} tableau from the slack basis, {el:.1f} s, {threads} threads "
+                      f"(this job's CPU share)",
             "pivot_sequence_matches_gpu": bool(ok and ok2),
+            "c_1thread": {"value": k1 / el1 if el1 > 0 else None, "pivots": k1,
+                          "seconds": el1},
             "numpy_1thread": {"value": k2 / el2, "pivots": k2, "seconds": el2,
                               "matches_gpu": bool(ok2)},
-            "host": {"cpu_count": os.cpu_count(),
-                     "OMP_NUM_THREADS": os.environ.get("OMP_NUM_THREADS"),
-                     "model": _cpu_model()}}
+            "host": _host_cpus()}
 
 
-def _cpu_model():
+def _host_cpus():
+    """Logical CPUs, sockets and physical cores of the host, this process's
+    CPU affinity and OMP_NUM_THREADS (/proc/cpuinfo, sched_getaffinity)."""
+    model, phys = None, set()
+    pid = cid = None
     try:
         for line in open("/proc/cpuinfo"):
-            if line.startswith("model name"):
-                return line.split(":", 1)[1].strip()
+            k, _, v = line.partition(":")
+            k, v = k.strip(), v.strip()
+            if k == "model name" and model is None:
+                model = v
+            elif k == "physical id":
+                pid = v
+            elif k == "core id":
+                cid = v
+            elif not k and pid is not None:
+                phys.add((pid, cid))
+                pid = cid = None
+        if pid is not None:
+            phys.add((pid, cid))
     except OSError:
         pass
-    return None
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        aff = None
+    return {"model": model, "logical_cpus": os.cpu_count(),
+            "sockets": len({p for p, _ in phys}) or None, "physical_cores": len(phys) or None,
+            "affinity_cpus": aff, "OMP_NUM_THREADS": os.environ.get("OMP_NUM_THREADS")}
+
+
+def peer_selftest(eng, world, rank, K, tdist, torch):
+    """Before the timed run: the row-sharded persistent chain must reproduce the
+    RCCL launch-per-phase path byte for byte on a small LP (every rank, all
+    ranks agree), else the bench falls back to RCCL.  Returns (ok, note)."""
+    from simplex_amd import synth
+    from simplex_amd.dist import row_partition
+    from simplex_amd.engine import SpxError
+
+    def all_ok(flag):
+        t = torch.tensor([1 if flag else 0], dtype=torch.int64)
+        tdist.all_reduce(t, op=tdist.ReduceOp.MIN)
+        return bool(t.item())
+
+    ms, ns = 256 * world, 2048
+    r0, r1 = row_partition(ms, world, rank)
+    T, obj, basis = synth.tableau_rows("dense", ms, ns, 99, r0, r1, order="F")
+    kw = dict(max_iters=4 * K + 5)
+    note = "ok"
+    try:
+        eng.set_chain(0)
+        eng.load_rows(T, obj, basis, ms, r0)
+        eng.enable_peer_chain()
+        ok = eng.chain_blocks() > 0
+        if ok:
+            eng.solve(**kw)
+            a = (eng.history().tobytes(), eng.tableau().tobytes())
+    except (SpxError, RuntimeError) as ex:
+        ok, note = False, f"peer chain failed: {ex}"
+    if not all_ok(ok):  # (every rank leaves here together: no collective is left pending)
+        return False, note if not ok else "peer chain failed on another rank"
+    eng.set_chain(1)  # the RCCL all-gather path on the same LP
+    eng.load_rows(T, obj, basis, ms, r0)
+    eng.solve(**kw)
+    same = (eng.history().tobytes(), eng.tableau().tobytes()) == a
+    eng.set_chain(0)
+    ok = all_ok(same)
+    return ok, "ok" if ok else "peer chain differs from the RCCL path: disabled"
 
 
 def main():
@@ -178,10 +252,20 @@ def main():
     K = 0 if K <= 1 else K
     if K:
         eng.set_window(K)
+    peer = None
+    if world > 1 and K and args.peer:
+        ok, note = peer_selftest(eng, world, rank, K, tdist, torch)
+        peer = {"enabled": ok, "selftest": note}
     if world == 1:
         eng.set_chain(args.chain, args.chain_blocks)
+    elif peer is None or not peer["enabled"]:
+        eng.set_chain(1)  # one RCCL all-gather per pivot
     eng.load_rows(Tf, obj, basis, m, row0)
     del Tf
+    if peer is not None and peer["enabled"]:
+        eng.enable_peer_chain()
+        if eng.chain_blocks() <= 0:
+            raise SystemExit("row-sharded persistent chain passed its self-test but does not fit")
     if args.nt >= 0 or args.ilv >= 0 or args.R or args.wgs or args.fmap >= 0:
         fmap = max(args.fmap, 0) & 3
         if args.ilv >= 0:
@@ -219,7 +303,7 @@ def main():
         raise SystemExit(f"pivot loop ended early: status {status}, iters {iters}")
     ms_tot, launches, touched = eng.elim_timing(reset=True)
     chain = None
-    if K and world == 1:
+    if K and (world == 1 or (peer and peer["enabled"])):
         # the pivot chain, the other half of a window: HIP events around each
         # window's chain in 8 windows AFTER the timed region (event nodes cost
         # stream time, so they stay out of `value`)
@@ -303,8 +387,14 @@ def main():
                        "step": (f"one tableau pass = a window of {K} pivots" if K
                                 else "one pivot (single-pivot elimination pass)"),
                        "window": K,
-                       "chain_blocks": eng.chain_blocks() if world == 1 else 0,
-                       "parallelism": f"row-shard x{world}" if world > 1 else "single GPU"},
+                       "chain_blocks": eng.chain_blocks(),
+                       "parallelism": ("single GPU" if world == 1 else
+                                       f"row-shard x{world}, " + (
+                                           "one persistent chain launch per window, ratio "
+                                           "records to every rank + peer row gather (xGMI)"
+                                           if peer and peer["enabled"] else
+                                           "RCCL all-gather of [key | row] per pivot")),
+                       "peer_chain": peer},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBPS,
                          "traffic": traffic,

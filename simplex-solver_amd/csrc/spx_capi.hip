@@ -408,6 +408,13 @@ int lazy_ratio_grid(const spx_ctx* ctx) {
   return std::max(1, (int)((ctx->m_local + BLK - 1) / BLK));
 }
 
+// Hardware queues of this process (HIP's GPU_MAX_HW_QUEUES, default 4).
+int hw_queues() {
+  const char* e = std::getenv("GPU_MAX_HW_QUEUES");
+  const int v = e ? std::atoi(e) : 0;
+  return v > 0 ? v : 4;
+}
+
 // Persistent chain geometry: B blocks of CB threads (one per CU, all
 // resident), each owning <= CB columns and <= CB rows.  Returns B (and CB in
 // *cb), or 0 when the chain does not apply (row shards, the launch-per-phase
@@ -435,9 +442,14 @@ int chain_blocks(spx_ctx* ctx, int* cb_out = nullptr, bool ignore_admission = fa
   const int64_t need = std::max<int64_t>({(ctx->N - 1 + cb - 1) / cb, (rows + cb - 1) / cb,
                                           1, (int64_t)ctx->chain_min_blocks});
   const int64_t cap = std::min<int64_t>((int64_t)ctx->n_cu, CHAIN_MAX_BLOCKS);
-  if (ctx->sharded)  // every rank's records in one poll; the chains sharing a GPU all resident
+  if (ctx->sharded) {  // every rank's records in one poll; the chains sharing a GPU all resident
+    // virtual ranks: one process's streams share its hardware queues
+    // (GPU_MAX_HW_QUEUES, 4 by default), and two chains on one queue run one
+    // after the other -- each would wait for the other's records forever
+    if (ctx->loop && ctx->peer_same_dev > hw_queues()) return 0;
     return need * ctx->nranks <= CHAIN_SH_SLOTS && need * ctx->peer_same_dev <= cap ? (int)need
                                                                                       : 0;
+  }
   return need <= cap ? (int)need : 0;
 }
 

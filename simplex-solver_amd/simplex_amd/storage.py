@@ -115,12 +115,15 @@ class StorageService:
     def save_json(data: Any, prefix: str, extension: str = ".json") -> Optional[str]:
         """Write ``data`` to a new sequential file; the path, or None on an I/O
         error (the reference prints the error and returns None, :76-88)."""
-        filename = StorageService._claim_next_filename(prefix, extension)
+        filename = None
         try:
+            # the claim creates OUTPUT_DIR and the name: an unwritable directory
+            # is an I/O error like any other (None, as the reference returns)
+            filename = StorageService._claim_next_filename(prefix, extension)
             _write_atomic(filename, data)
             return filename
         except (IOError, OSError) as e:
-            print(f"Error al guardar el archivo {filename}: {e}")
+            print(f"Error al guardar el archivo {filename or prefix}: {e}")
             return None
 
     @staticmethod
@@ -189,6 +192,11 @@ def _write_atomic(path: str, data: Any) -> None:
     d = os.path.dirname(path) or "."
     fd, tmp = tempfile.mkstemp(prefix=".tmp_", suffix=".json", dir=d)
     try:
+        # mkstemp creates 0600; the report keeps the mode a plain open() gives
+        # (0666 & ~umask), as the reference's json.dump target has
+        umask = os.umask(0)
+        os.umask(umask)
+        os.fchmod(fd, 0o666 & ~umask)
         with os.fdopen(fd, "w", encoding="utf-8") as f:
             _dump(data, f, 0)
             f.write("\n")

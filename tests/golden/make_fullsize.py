@@ -38,8 +38,16 @@ JSON = os.path.join(HERE, "fullsize.json")
 CONFIGS = {
     "config3": dict(kind="dense", m=8192, n=8192, seed=20251205, rule="dantzig",
                     checkpoints=[24, 240, 2400]),
+    # Bland on this degenerate generator stalls at the degenerate origin: no
+    # improving pivot in 7.3M GPU pivots (profiles/r03/config5_bland_probe.log),
+    # while HiGHS finds z* > 0.  Config 5 is pinned over a 100k-pivot prefix;
+    # the same generator at 128 and 256 rows terminates and is pinned to
+    # optimality (degen128 / degen256).
     "config5": dict(kind="degenerate", m=4096, n=4096, seed=5, rule="bland",
-                    checkpoints=[24, 240, 2400]),
+                    checkpoints=[24, 240, 2400, 24000], max_pivots=100000),
+    "degen128": dict(kind="degenerate", m=128, n=128, seed=5, rule="bland", checkpoints=[24]),
+    "degen256": dict(kind="degenerate", m=256, n=256, seed=5, rule="bland",
+                     checkpoints=[24, 2400]),
 }
 
 
@@ -71,9 +79,12 @@ def oracle_solve(name: str) -> dict:
     t0 = time.perf_counter()
     chunk = 24
     status = 1
-    while status == 1:
+    cap = cfg.get("max_pivots", 0)
+    while status == 1 and (not cap or len(hist) < cap):
         nxt = min([k for k in cfg["checkpoints"] if k > len(hist)] or [len(hist) + 2400])
         want = min(chunk, nxt - len(hist))
+        if cap:
+            want = min(want, cap - len(hist))
         status, h = C.solve(T, basis, rule=cfg["rule"], max_iters=want, hist_cap=want)
         hist += h
         if len(hist) in cfg["checkpoints"] and status == 1:
@@ -84,15 +95,50 @@ def oracle_solve(name: str) -> dict:
         chunk = 240
     el = time.perf_counter() - t0
     h = np.asarray(hist, dtype=np.int32).reshape(-1, 2)
+    b0 = np.arange(cfg["n"], cfg["n"] + cfg["m"], dtype=np.int64)  # the slack basis
+    reps = zobrist_repeats(h.astype(np.int64), b0)
     np.savez_compressed(os.path.join(HERE, f"fullsize_{name}.npz"), hist=h,
                         basis=basis.astype(np.int32))
     out = dict(cfg, status=int(status), pivots=len(hist), objective=float(T[-1, -1]),
                objective_hex=float(T[-1, -1]).hex(), tableau_sha256=digest(T),
                checkpoint_sha256=cps, oracle_seconds=el, oracle_threads=C.threads(),
+               basis_repeats=reps,
                generator="tests/golden/make_fullsize.py (oracle/spx_oracle.c, skip_zero)")
     print(f"{name}: status {status}, {len(hist)} pivots in {el:.0f} s, z = {T[-1, -1]!r}",
           flush=True)
     return out
+
+
+def _key(r: np.ndarray, v: np.ndarray) -> np.ndarray:
+    """Zobrist key of (row, variable): splitmix64 of a packed index."""
+    with np.errstate(over="ignore"):
+        z = (r.astype(np.uint64) << np.uint64(32)) + v.astype(np.uint64) + np.uint64(0x9E3779B97F4A7C15)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        return z ^ (z >> np.uint64(31))
+
+
+def zobrist_repeats(hist: np.ndarray, basis0: np.ndarray) -> int:
+    """Bases revisited along a pivot sequence (0: no cycle).  A basis hashes to
+    the XOR of a key per (row, basic variable); pivot k at row r swaps the key
+    of r's previous variable (the last earlier pivot at r, else basis0[r]) for
+    that of c_k, so the hash after every pivot is a running XOR (vectorised)."""
+    hist = np.asarray(hist, dtype=np.int64).reshape(-1, 2)
+    basis0 = np.asarray(basis0, dtype=np.int64)
+    h0 = np.bitwise_xor.reduce(_key(np.arange(basis0.shape[0]), basis0))
+    if len(hist) == 0:
+        return 0
+    r, c = hist[:, 0], hist[:, 1]
+    order = np.lexsort((np.arange(len(r)), r))  # by row, then pivot order
+    prev = basis0[r].copy()
+    rs, cs = r[order], c[order]
+    same = np.r_[False, rs[1:] == rs[:-1]]
+    prev_sorted = np.where(same, np.r_[0, cs[:-1]], basis0[rs])
+    prev[order] = prev_sorted
+    delta = _key(r, prev) ^ _key(r, c)
+    hs = np.bitwise_xor.accumulate(delta) ^ h0
+    allh = np.r_[np.uint64(h0), hs]
+    return int(len(allh) - len(np.unique(allh)))
 
 
 def highs(name: str, time_limit: float = 3000.0) -> dict:
@@ -112,10 +158,11 @@ def highs(name: str, time_limit: float = 3000.0) -> dict:
 
 
 def main(argv):
-    todo = argv or ["config3", "config5", "highs3", "highs5"]
+    todo = argv or ["config3", "config5", "degen128", "degen256", "highs3", "highs5",
+                    "highsdegen128", "highsdegen256"]
     for what in todo:
         if what.startswith("highs"):
-            name = "config" + what[5:]
+            name = what[5:] if what[5:].startswith("degen") else "config" + what[5:]
             res = highs(name)
         else:
             name = what

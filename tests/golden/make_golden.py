@@ -43,10 +43,12 @@ TEXTBOOK = [
     dict(name="wyndor", cite="tests/test_visualization_integration.py:38-56", maximize=True,
          c=[3, 5], rows=[([1, 0], "<=", 4), ([0, 2], "<=", 12), ([3, 2], "<=", 18)],
          ref_answer=dict(z=36.0, x=[2.0, 6.0])),
+    # the reference test holds Z = 30 only; its mocked x = (5, 3, 2) is not an
+    # optimum (:447-452), so x is HiGHS's, kept apart as highs_x
     dict(name="three_var", cite="tests/test_visualization_integration.py:417-444 (config 1)",
          maximize=True, c=[1, 2, 3],
          rows=[([1, 1, 1], "<=", 10), ([2, 1, 0], "<=", 15), ([0, 2, 1], "<=", 12)],
-         ref_answer=dict(z=30.0, x=[0.0, 0.0, 10.0])),
+         ref_answer=dict(z=30.0), highs_x=[0.0, 0.0, 10.0]),
     dict(name="equality", cite="tests/test_visualization_integration.py:205-224", maximize=True,
          c=[1, 1], rows=[([1, 1], "=", 10), ([2, 1], "<=", 15)], ref_answer=dict(z=10.0)),
     dict(name="infeasible", cite="tests/test_visualization_integration.py:240-259",
@@ -126,6 +128,8 @@ def textbook():
             if "status" in ref:
                 assert bl["status"] == ref["status"], case["name"]
         entry["ref_answer"] = ref
+        if "highs_x" in case:  # an x from HiGHS, not from the reference tests
+            entry["highs"]["x"] = case["highs_x"]
         out.append(entry)
     return out
 

@@ -40,9 +40,12 @@ def _digest(T):
 
 
 def _full_solve(name, window=24):
+    """The fixture's solve on the GPU: to optimality, or over the fixture's
+    pivot prefix (max_pivots, status 1) when the oracle run was capped."""
     from simplex_amd import synth
     from simplex_amd.engine import DeviceTableau
     fx, hist, basis_end = _fixture(name)
+    cap = fx.get("max_pivots", 0)
     Tf, obj, basis = synth.tableau_rows(fx["kind"], fx["m"], fx["n"], fx["seed"], order="F")
     with DeviceTableau(0) as e:
         e.set_window(window)
@@ -54,16 +57,16 @@ def _full_solve(name, window=24):
             assert r.status == 1 and r.iters == k - done
             done = k
             assert _digest(e.tableau()) == fx["checkpoint_sha256"][str(k)], f"after {k} pivots"
-        res = e.solve(rule=fx["rule"])
+        res = e.solve(rule=fx["rule"], max_iters=(cap - done) if cap else 0)
         h = e.history()
-        assert res.status == fx["status"] == 0
+        assert res.status == fx["status"] == (1 if cap else 0)
         assert done + res.iters == fx["pivots"] == len(h)
         assert np.array_equal(h, hist), "pivot sequence differs from the oracle"
         assert np.array_equal(e.basis(), basis_end)
         z = res.objective
         assert z == fx["objective"], (z, fx["objective"])
         assert _digest(e.tableau()) == fx["tableau_sha256"]
-    if fx.get("highs_status") == 0:
+    if fx.get("highs_status") == 0 and not cap:
         hz = fx["highs_objective"]
         assert abs(z - hz) <= 1e-9 * max(1.0, abs(hz)), (z, hz)
     return fx
@@ -75,10 +78,44 @@ def test_config3_dantzig_full_solve_pinned():
     _full_solve("config3")
 
 
-def test_config5_bland_full_solve_pinned():
-    """Config 5 (4096 x 4096 degenerate LP, Bland): anti-cycling to
-    optimality, every basis index of the oracle's sequence."""
-    _full_solve("config5")
+def test_config5_bland_100k_pivots_pinned():
+    """Config 5 (4096 x 4096 degenerate LP, Bland): the first 100,000 pivots
+    (Bland stalls at the degenerate origin far longer on this generator,
+    profiles/r03/config5_bland_probe.log), every index and the tableau digests
+    of the oracle's; the oracle's run revisits no basis (fixture)."""
+    fx = _full_solve("config5")
+    assert fx["basis_repeats"] == 0
+
+
+@pytest.mark.parametrize("name", ["degen128", "degen256"])
+def test_degenerate_bland_to_optimality_pinned(name):
+    """The config-5 generator at 128 and 256 rows, where Bland terminates
+    (7,604 and 56,262 pivots, almost all degenerate): to optimality, every
+    index, the final tableau's digest, the objective within 1e-9 of HiGHS."""
+    fx = _full_solve(name, window=8)
+    assert fx["basis_repeats"] == 0
+
+
+def test_config5_bland_million_pivots_no_basis_repeats():
+    """Anti-cycling at full size: 2^20 Bland pivots of config 5 on the GPU
+    (K = 24) revisit no basis (Zobrist hashes of every basis along the
+    recorded history), and their first 100,000 are the oracle's."""
+    from simplex_amd import synth
+    from simplex_amd.engine import DeviceTableau
+    import sys
+    sys.path.insert(0, GOLD)
+    from make_fullsize import zobrist_repeats
+    fx, hist, _ = _fixture("config5")
+    T, basis = synth.full_tableau("degenerate", 4096, 4096, 5)
+    with DeviceTableau(0) as e:
+        e.set_window(24)
+        e.load(T, basis)
+        del T
+        r = e.solve(rule="bland", max_iters=1 << 20)
+        assert r.status == 1 and r.iters == 1 << 20
+        h = e.history()
+    assert np.array_equal(h[:len(hist)], hist)
+    assert zobrist_repeats(h, basis) == 0
 
 
 @pytest.mark.parametrize("window", [24])

@@ -272,3 +272,23 @@ def test_storage_concurrent_saves_unique_and_complete(tmp_path, monkeypatch):
     ks = sorted(json.load(open(p, encoding="utf-8"))["k"] for p in paths)
     assert ks == list(range(32))
     assert not [f for f in os.listdir(tmp_path) if f.startswith(".tmp_")]
+
+
+def test_storage_report_mode_and_unwritable_dir(tmp_path, monkeypatch):
+    """Saved reports keep the mode a plain open() gives (0666 & ~umask), and an
+    unusable OUTPUT_DIR makes save_json return None instead of raising
+    (reference storage_service.py:76-88 prints the error and returns None)."""
+    import os
+    import stat
+    from simplex_amd import storage
+    monkeypatch.setattr(storage, "OUTPUT_DIR", str(tmp_path))
+    old = os.umask(0o022)
+    try:
+        path = storage.StorageService.save_solution({"a": 1})
+    finally:
+        os.umask(old)
+    assert stat.S_IMODE(os.stat(path).st_mode) == 0o644
+    blocker = tmp_path / "not_a_dir"
+    blocker.write_text("x")
+    monkeypatch.setattr(storage, "OUTPUT_DIR", str(blocker / "sub"))
+    assert storage.StorageService.save_solution({"a": 1}) is None

@@ -140,3 +140,48 @@ def test_c_oracle_bit_identical_to_numpy_oracle(kind, m, n, seed, rule, skip):
     st2, h2 = C.solve(T2, b2, rule=rule, skip_zero=skip)
     assert st == st2 and h == h2 and np.array_equal(b, b2)
     assert T.tobytes() == T2.tobytes()
+
+
+# ----------------------------------------------------------- full-size fixtures
+def _fullsize():
+    import json
+    import os
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "fullsize.json")
+    if not os.path.exists(path):
+        pytest.skip("fullsize.json not generated")
+    return json.load(open(path))
+
+
+def test_fullsize_fixtures_consistent_with_highs_and_acyclic():
+    """The oracle's full-size runs (tests/golden/make_fullsize.py) agree with
+    HiGHS (the reference's answer path, solver_controller.py:76-85) within
+    1e-9 wherever they reached optimality, and revisit no basis."""
+    import os
+    fx = _fullsize()
+    here = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+    for name, f in fx.items():
+        if "pivots" not in f:
+            continue
+        z = np.load(os.path.join(here, f"fullsize_{name}.npz"))
+        assert z["hist"].shape == (f["pivots"], 2)
+        assert f.get("basis_repeats", 0) == 0
+        if f["status"] == 0 and f.get("highs_status") == 0:
+            hz = f["highs_objective"]
+            assert abs(f["objective"] - hz) <= 1e-9 * max(1.0, abs(hz)), name
+            assert float.fromhex(f["objective_hex"]) == f["objective"]
+
+
+def test_zobrist_detects_a_revisited_basis():
+    """The cycle detector itself: Beale's LP under Dantzig revisits its first
+    basis after 6 pivots."""
+    import os
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden"))
+    from make_fullsize import zobrist_repeats
+    sf = O.standard_form([0.75, -20, 0.5, -6],
+                         [([0.25, -8, -1, 9], "<=", 0), ([0.5, -12, -0.5, 3], "<=", 0),
+                          ([0, 0, 1, 0], "<=", 1)], True)
+    T, b = sf["T"], sf["basis"].copy()
+    b0 = b.copy()
+    st, h = O.solve_tableau(T, b, rule="dantzig", max_iters=12)
+    assert st == 1 and zobrist_repeats(np.asarray(h, dtype=np.int64), b0) > 0

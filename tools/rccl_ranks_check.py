@@ -1,7 +1,7 @@
 """Multi-process check of the row-sharded pivot path.
 
 Launch: python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 \\
-        tools/rccl_ranks_check.py [--m M --n N --pivots K --window K --peer P --same-device]
+        tools/rccl_ranks_check.py [--rows M --cols N --pivots K --window K --peer P --same-device]
 Every rank loads its row block and runs the pivots, then rank 0 checks every
 rank's rows, the objective row and the pivot sequence against the CPU oracle
 (bit-exact) and exits non-zero on a mismatch.
@@ -11,7 +11,8 @@ rank's rows, the objective row and the pivot sequence against the CPU oracle
   --peer 2  no communicator at all: the persistent chain's peers only
             (spx_create_sharded_peer; works with several ranks on one GPU,
             which RCCL refuses)
---same-device puts all ranks on GPU 0.
+--same-device puts all ranks on GPU 0.  (--rows / --cols: torch.distributed.run
+would take --m / --n as abbreviations of its own options.)
 """
 import argparse
 import os
@@ -27,8 +28,8 @@ import torch.distributed as dist  # noqa: E402
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--m", type=int, default=300)
-    ap.add_argument("--n", type=int, default=500)
+    ap.add_argument("--rows", type=int, default=300)
+    ap.add_argument("--cols", type=int, default=500)
     ap.add_argument("--pivots", type=int, default=0)
     ap.add_argument("--window", type=int, default=0)
     ap.add_argument("--peer", type=int, default=0, choices=[0, 1, 2])
@@ -42,15 +43,15 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", rank))
     from simplex_amd import dist as sdist, synth
     dev = 0 if a.same_device else local
-    r0, r1 = sdist.row_partition(a.m, world, rank)
-    T, obj, basis = synth.tableau_rows(a.kind, a.m, a.n, a.seed, r0, r1, order="F")
+    r0, r1 = sdist.row_partition(a.rows, world, rank)
+    T, obj, basis = synth.tableau_rows(a.kind, a.rows, a.cols, a.seed, r0, r1, order="F")
     if a.peer == 2:
         s = sdist.ShardedTableau(dev, rank, world, local="peer")
     else:
         s = sdist.ShardedTableau(dev, rank, world, sdist.exchange_unique_id())
     with s:
         s.set_window(a.window)
-        s.load_shard(T, obj, basis, a.m, r0)
+        s.load_shard(T, obj, basis, a.rows, r0)
         if a.peer:
             s.enable_peer_chain()
         blocks = s.chain_blocks()
@@ -61,7 +62,7 @@ def main():
     ok = True
     if rank == 0:
         from oracle import simplex_oracle as O
-        Tf, bf = synth.full_tableau(a.kind, a.m, a.n, a.seed)
+        Tf, bf = synth.full_tableau(a.kind, a.rows, a.cols, a.seed)
         st, hist = O.solve_tableau(Tf, bf, rule=a.rule, max_iters=a.pivots)
         for q, (r0, r1, stq, h, Tl, b, nb) in enumerate(outs):
             good = ([tuple(x) for x in h] == hist and np.array_equal(Tl[:-1], Tf[r0:r1])
