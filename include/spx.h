@@ -16,10 +16,11 @@
  *    keeps a host pointer after a call returns.  A context owns all device
  *    memory (and the RCCL communicator of a sharded context); spx_destroy
  *    frees it.
- *  - Re-entrant: no global mutable state.  One context per solve, one HIP
- *    stream per context; distinct contexts may be used from distinct threads
- *    concurrently (the reference's /solve is entered from many threads,
- *    tests/test_performance_load.py:80-83).
+ *  - Re-entrant: no global mutable state besides two mutex-guarded registries
+ *    (virtual-rank groups, persistent-chain admission per device).  One
+ *    context per solve, one HIP stream per context; distinct contexts may be
+ *    used from distinct threads concurrently (the reference's /solve is
+ *    entered from many threads, tests/test_performance_load.py:80-83).
  *  - Tableau (the spec): rows 0..m-1 are constraints, the
  *    objective row is logically row m ("z_j - c_j" form of a MAX problem, RHS
  *    = current objective value).  Columns 0..N-2 are variables, column N-1 is

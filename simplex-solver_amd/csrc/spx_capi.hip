@@ -151,6 +151,7 @@ struct spx_ctx {
   bool peer_ok = false;
   ChainPeers peers{};
   std::vector<void*> ipc_open;  // IPC-mapped peer buffers (closed on reload / destroy)
+  ChainPeers* d_peers = nullptr;  // device copy of `peers` (the chain kernel's argument)
   int peer_same_dev = 1;        // ranks whose chains share this rank's GPU
 
   // graph cache
@@ -565,12 +566,11 @@ int enqueue_window_t(spx_ctx* ctx, int npiv, bool time_flush) {
     auto kern = ctx->sharded ? (cb == 512 ? chain_kernel<KMAX, 512, true>
                                           : chain_kernel<KMAX, 256, true>)
                              : (cb == 512 ? chain_kernel<KMAX, 512> : chain_kernel<KMAX, 256>);
-    ChainPeers pe = ctx->peers;
-    pe.stop_req = (const int32_t*)ctx->d_stop;
     hipLaunchKernelGGL(kern, dim3(B), dim3(cb), 0, ctx->stream, ctx->enter_part, ctx->st,
                        (const Params*)ctx->prm, std::max(NWAVE * ctx->nbn, B),
                        (const double*)ctx->A, ctx->ld, ctx->m_local, ctx->N, ctx->obj, ctx->win,
-                       npiv, ctx->basis, ctx->hist, ctx->gr_enter, ctx->gr_ratio, cpb, rpb, pe);
+                       npiv, ctx->basis, ctx->hist, ctx->gr_enter, ctx->gr_ratio, cpb, rpb,
+                       (const ChainPeers*)ctx->d_peers);
   } else if (ctx->sharded && !ctx->comm && !ctx->loop) {
     ctx->err = "a peer-only shard needs the persistent chain (windowed, spx_peer_import done, "
                "chain mode != 1, and its grid fits)";
@@ -637,9 +637,7 @@ int enqueue_window_t(spx_ctx* ctx, int npiv, bool time_flush) {
     const int rc = record_event(ctx, e->second);
     if (rc) return rc;
   }
-  // the fast-path columns' leaving rows (every window: partial ones included)
-  hipLaunchKernelGGL(row_fix_kernel<KMAX>, dim3(ctx->nbn), dim3(BLK), 0, ctx->stream, ctx->A,
-                       ctx->ld, ctx->m_local, ctx->row0, ctx->N, ctx->win, npiv);
+  // (the fast-path columns' leaving rows: the flush's tail, spx_delayed.hpp)
   HIPC(hipGetLastError());
   return SPX_OK;
 }
@@ -1012,6 +1010,20 @@ struct PeerBlob {
 };
 constexpr uint32_t PEER_MAGIC = 0x53505850u;  // "SPXP"
 
+// Install a peers table: host copy, device copy (with this rank's stop word), on.
+int peer_commit(spx_ctx* ctx, const ChainPeers& pe, int same_dev) {
+  ctx->peers = pe;
+  ctx->peers.stop_req = (const int32_t*)ctx->d_stop;
+  if (!ctx->d_peers) HIPC(hipMalloc(&ctx->d_peers, sizeof(ChainPeers)));
+  HIPC(hipMemcpyAsync(ctx->d_peers, &ctx->peers, sizeof(ChainPeers), hipMemcpyHostToDevice,
+                      ctx->stream));
+  HIPC(hipStreamSynchronize(ctx->stream));
+  ctx->peer_same_dev = same_dev;
+  ctx->peer_ok = true;
+  drop_graphs(ctx);
+  return SPX_OK;
+}
+
 int peer_check(spx_ctx* ctx) {
   CHECK_ARG(ctx->sharded && ctx->loaded, "peer chain: a loaded sharded context is needed");
   CHECK_ARG(ctx->nranks <= CHAIN_MAX_RANKS, "peer chain: at most 16 ranks");
@@ -1092,11 +1104,7 @@ int spx_peer_import(spx_ctx* ctx, const void* blobs, int nranks) {
     pe.A[q] = static_cast<const double*>(pa);
     pe.ratio[q] = static_cast<unsigned long long*>(pr);
   }
-  ctx->peers = pe;
-  ctx->peer_same_dev = same;
-  ctx->peer_ok = true;
-  drop_graphs(ctx);
-  return SPX_OK;
+  return peer_commit(ctx, pe, same);
 }
 
 // Virtual ranks (spx_create_sharded_local): the peers are this process's
@@ -1124,11 +1132,7 @@ int spx_peer_chain_local(spx_ctx* ctx) {
   }
   if (!G->barrier()) return loop_fail(ctx);  // nobody reloads while the others read
   close_peers(ctx);
-  ctx->peers = pe;
-  ctx->peer_same_dev = same;
-  ctx->peer_ok = true;
-  drop_graphs(ctx);
-  return SPX_OK;
+  return peer_commit(ctx, pe, same);
 }
 
 int spx_destroy(spx_ctx* ctx) {
@@ -1160,6 +1164,7 @@ int spx_destroy(spx_ctx* ctx) {
   if (ctx->h_st) (void)hipHostFree(ctx->h_st);
   if (ctx->h_poll) (void)hipHostFree(ctx->h_poll);
   if (ctx->h_stop) (void)hipHostFree(ctx->h_stop);
+  dfree(ctx->d_peers);
   for (hipEvent_t ev : ctx->ev_poll)
     if (ev) (void)hipEventDestroy(ev);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);

@@ -442,7 +442,7 @@ __global__ __launch_bounds__(CB) void chain_kernel(
     const double* __restrict__ A, int64_t ld, int64_t m, int64_t N, double* __restrict__ obj,
     Window win, int npiv, int64_t* __restrict__ basis, int64_t* __restrict__ hist,
     unsigned long long* gr_enter_, unsigned long long* gr_ratio_, int cpb, int rpb,
-    ChainPeers pe) {
+    const ChainPeers* __restrict__ pep) {
   static_assert(KMAX <= 32, "slots are lane-indexed and fit the window buffers");
   constexpr int NW = CB / 64;
   constexpr int CH = KMAX % 8 == 0 ? 8 : KMAX % 4 == 0 ? 4 : 2;
@@ -487,19 +487,22 @@ __global__ __launch_bounds__(CB) void chain_kernel(
   const int64_t iter_limit = prm->iter_limit;
   const bool skip = prm->skip_zero != 0;
   const uint32_t W = (E + 1u) & TAG_EPOCH;  // this window's epoch (the same on every rank)
+  // SH: the peers' table lives in device memory (a by-value kernel argument of
+  // this size measurably slowed the single-GPU chain); unused otherwise
+  const ChainPeers* pe = pep;
   // row shards: my rank's rows start at row0; the ratio records of all nr * B
   // blocks are polled (block slot rank * B + b, planes RS apart)
-  const int rank = SH ? pe.rank : 0;
-  const int nr = SH ? pe.nranks : 1;
-  const int64_t row0 = SH ? pe.row0[rank] : 0;
+  const int rank = SH ? pe->rank : 0;
+  const int nr = SH ? pe->nranks : 1;
+  const int64_t row0 = SH ? pe->row0[rank] : 0;
   constexpr int RS = SH ? CHAIN_SH_SLOTS : CHAIN_MAX_BLOCKS;
   const int BR = SH ? nr * B : B;
   const int bs = SH ? rank * B + b : b;
   // rank 0's time-limit stop request rides in its ratio records (bit 31 of
   // granule 3); read once per window, so every rank stops at the window's start
   const unsigned stopbit =
-      (SH && rank == 0 && pe.stop_req &&
-       __hip_atomic_load(const_cast<int32_t*>(pe.stop_req), __ATOMIC_RELAXED,
+      (SH && rank == 0 && pe->stop_req &&
+       __hip_atomic_load(const_cast<int32_t*>(pe->stop_req), __ATOMIC_RELAXED,
                          __HIP_MEMORY_SCOPE_SYSTEM) != 0)
           ? 1u : 0u;
   // the ratio buffer of pivot it0 + q: SH alternates two halves by pivot
@@ -507,7 +510,7 @@ __global__ __launch_bounds__(CB) void chain_kernel(
   // q + 1 before a peer has read ratio q; never q + 2)
   auto ratio_buf = [&](int d, int qq) -> gu64* {
     if constexpr (SH)
-      return (gu64*)pe.ratio[d] + (size_t)((it0 + qq) & 1) * RATIO_REC * RS;
+      return (gu64*)pe->ratio[d] + (size_t)((it0 + qq) & 1) * RATIO_REC * RS;
     else
       return gr_ratio;
   };
@@ -717,7 +720,7 @@ __global__ __launch_bounds__(CB) void chain_kernel(
                                    stopbit);
       SPX_PROBE_CHAIN(q, 0);
     }
-    // f_q for the flush / row_fix (later kernels): stored after the record, so
+    // f_q for the flush (a later kernel): stored after the record, so
     // these stores never queue in front of it
     if (ilive) win.F[(int64_t)q * ld + i] = fv;
     SPX_PROBE(q, 0, 3, true);
@@ -757,7 +760,7 @@ __global__ __launch_bounds__(CB) void chain_kernel(
     if constexpr (SH) {  // the owner's stale row (a peer's tableau unless it is mine)
       const int own = wb / B;
       if (own == rank) v = A[jc * ld + (r - row0)];
-      else v = sys_load(pe.A[own] + jc * pe.ld[own] + (r - pe.row0[own]));
+      else v = sys_load(pe->A[own] + jc * pe->ld[own] + (r - pe->row0[own]));
     } else {
       v = A[jc * ld + r];
     }
@@ -905,7 +908,7 @@ __global__ __launch_bounds__(CB) void chain_kernel(
       SPX_PROBE_CHAIN(q, 2);
     }
     // stores for later kernels, after the record (never queued in front of it):
-    // the pivot's bookkeeping (the flush and row_fix read p from the records)
+    // the pivot's bookkeeping (the flush reads p from the records)
     if (b == 0 && t == CB - 1) {  // block 0's last thread: not in the polling wave
       st->r = r;
       st->c = c;
@@ -924,7 +927,7 @@ __global__ __launch_bounds__(CB) void chain_kernel(
     SPX_PROBE(q, 1, 3, true);
   }
   if constexpr (SH) {
-    // Window-end barrier: a rank's next kernels (flush, row_fix) rewrite its
+    // Window-end barrier: a rank's next kernel (the flush) rewrites its
     // rows, so none may start while a peer still gathers one of them.  Every
     // block reports once its last row gather has returned (its values were
     // consumed before the last block barrier above); block 0 of every rank
@@ -933,9 +936,9 @@ __global__ __launch_bounds__(CB) void chain_kernel(
     if (w0) {
       const unsigned dtag = rec_tag(W, 0, GK_DONE);
       if (lane < nr)
-        g_store<true>((gu64*)pe.ratio[lane] + (size_t)2 * RATIO_REC * RS + bs, dtag, 0u);
+        g_store<true>((gu64*)pe->ratio[lane] + (size_t)2 * RATIO_REC * RS + bs, dtag, 0u);
       if (b == 0) {
-        const gu64* dp = (const gu64*)pe.ratio[rank] + (size_t)2 * RATIO_REC * RS;
+        const gu64* dp = (const gu64*)pe->ratio[rank] + (size_t)2 * RATIO_REC * RS;
         for (unsigned spins = 0;;) {
           bool ok = true;
           for (int x = lane; x < BR; x += 64) ok &= (unsigned)(g_load<true>(dp + x) >> 32) == dtag;

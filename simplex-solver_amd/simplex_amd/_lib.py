@@ -137,8 +137,15 @@ def lib() -> ctypes.CDLL:
             handle = ctypes.CDLL(LIB_PATH)
         except OSError as e:  # pragma: no cover - environment dependent
             raise SpxLibraryError(f"cannot load {LIB_PATH}: {e}") from e
+        # SPX_LIB_PARTIAL=1: tolerate symbols an older build lacks (same-box
+        # A/B of two library builds only; the product binds everything)
+        partial = os.environ.get("SPX_LIB_PARTIAL") == "1"
         for name, (res, args) in SIGNATURES.items():
-            fn = getattr(handle, name)
+            fn = getattr(handle, name, None)
+            if fn is None:
+                if partial:
+                    continue
+                raise SpxLibraryError(f"{LIB_PATH} lacks {name}")
             fn.restype = res
             fn.argtypes = args
         if handle.spx_abi_version() != 1:
