@@ -446,8 +446,11 @@ int chain_blocks(spx_ctx* ctx, int* cb_out = nullptr, bool ignore_admission = fa
   if (ctx->sharded) {  // every rank's records in one poll; the chains sharing a GPU all resident
     // virtual ranks: one process's streams share its hardware queues
     // (GPU_MAX_HW_QUEUES, 4 by default), and two chains on one queue run one
-    // after the other -- each would wait for the other's records forever
-    if (ctx->loop && ctx->peer_same_dev > hw_queues()) return 0;
+    // after the other -- each would wait for the other's records forever.  One
+    // queue stays for the process's other streams (the default stream once
+    // used, other contexts): with 4 virtual ranks beside it, two ranks' chains
+    // shared a queue and timed out (round 3)
+    if (ctx->loop && ctx->peer_same_dev >= hw_queues()) return 0;
     return need * ctx->nranks <= CHAIN_SH_SLOTS && need * ctx->peer_same_dev <= cap ? (int)need
                                                                                       : 0;
   }
@@ -563,8 +566,8 @@ int enqueue_window_t(spx_ctx* ctx, int npiv, bool time_flush) {
   if (B > 0) {
     const int cpb = (int)((ctx->N - 1 + B - 1) / B);  // (B * cpb == N-1: xown owns the RHS)
     const int rpb = (int)std::max<int64_t>(1, (ctx->m_local + B - 1) / B);
-    auto kern = ctx->sharded ? (cb == 512 ? chain_kernel<KMAX, 512, true>
-                                          : chain_kernel<KMAX, 256, true>)
+    auto kern = ctx->sharded ? (cb == 512 ? chain_shard_kernel<KMAX, 512>
+                                          : chain_shard_kernel<KMAX, 256>)
                              : (cb == 512 ? chain_kernel<KMAX, 512> : chain_kernel<KMAX, 256>);
     hipLaunchKernelGGL(kern, dim3(B), dim3(cb), 0, ctx->stream, ctx->enter_part, ctx->st,
                        (const Params*)ctx->prm, std::max(NWAVE * ctx->nbn, B),
@@ -637,7 +640,10 @@ int enqueue_window_t(spx_ctx* ctx, int npiv, bool time_flush) {
     const int rc = record_event(ctx, e->second);
     if (rc) return rc;
   }
-  // (the fast-path columns' leaving rows: the flush's tail, spx_delayed.hpp)
+  // the fast-path columns' leaving rows (every window: partial ones included);
+  // a tail inside the flush measured 226 vs 182 us (profiles/r03/ab_chain2)
+  hipLaunchKernelGGL(row_fix_kernel<KMAX>, dim3(ctx->nbn), dim3(BLK), 0, ctx->stream, ctx->A,
+                       ctx->ld, ctx->m_local, ctx->row0, ctx->N, ctx->win, npiv);
   HIPC(hipGetLastError());
   return SPX_OK;
 }

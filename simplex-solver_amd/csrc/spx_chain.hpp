@@ -72,7 +72,7 @@ constexpr int RATIO_HDR = 4;            // v_lo, v_hi, row, t (t read under Blan
 constexpr int RATIO_REC = RATIO_HDR + 2 + 2 * 32;  // + RHS of row (lo, hi), f_0..f_q[row]
 constexpr int CHAIN_MAX_BLOCKS = 256;   // one block per CU
 constexpr unsigned CHAIN_SPIN_MAX = 1u << 22;
-// Row-sharded chain (chain_kernel<.., SH = true>): the ratio
+// Row-sharded chain (chain_shard_kernel): the ratio
 // records of every rank's blocks land in every rank's buffer, at block slot
 // rank * B + b of planes CHAIN_SH_SLOTS apart; two halves by pivot parity, then
 // one plane of window-end granules.
@@ -268,8 +268,8 @@ __device__ __forceinline__ void decode_record(KeyP& k, const unsigned long long 
   }
 }
 
-template <bool RATIO, int G, int RPL, bool SYS>
-__device__ __forceinline__ bool poll_records_n(const gu64* recs, int B, int rs, unsigned tag,
+template <bool RATIO, int G, int RPL, bool SYS, int rs>
+__device__ __forceinline__ bool poll_records_n(const gu64* recs, int B, unsigned tag,
                                                int rule, KeyP& k, State* st, bool* stop) {
   const int lane = threadIdx.x & 63;
   // lane l reads blocks l, l+64, ... (RPL records): every load of a pass is
@@ -310,23 +310,23 @@ __device__ __forceinline__ bool poll_records_n(const gu64* recs, int B, int rs, 
   return true;
 }
 
-template <bool RATIO, int G, bool SYS = false>
-__device__ __forceinline__ bool poll_records(const gu64* recs, int B, int rs, unsigned tag,
+template <bool RATIO, int G, bool SYS = false, int rs = CHAIN_MAX_BLOCKS>
+__device__ __forceinline__ bool poll_records(const gu64* recs, int B, unsigned tag,
                                              int rule, KeyP& k, State* st,
                                              bool* stop = nullptr) {
-  if (B <= 64) return poll_records_n<RATIO, G, 1, SYS>(recs, B, rs, tag, rule, k, st, stop);
-  if (B <= 128) return poll_records_n<RATIO, G, 2, SYS>(recs, B, rs, tag, rule, k, st, stop);
+  if (B <= 64) return poll_records_n<RATIO, G, 1, SYS, rs>(recs, B, tag, rule, k, st, stop);
+  if (B <= 128) return poll_records_n<RATIO, G, 2, SYS, rs>(recs, B, tag, rule, k, st, stop);
   if (!SYS || B <= 256)
-    return poll_records_n<RATIO, G, 4, SYS>(recs, B, rs, tag, rule, k, st, stop);
-  return poll_records_n<RATIO, G, 8, SYS>(recs, B, rs, tag, rule, k, st, stop);
+    return poll_records_n<RATIO, G, 4, SYS, rs>(recs, B, tag, rule, k, st, stop);
+  return poll_records_n<RATIO, G, 8, SYS, rs>(recs, B, tag, rule, k, st, stop);
 }
 
 // The dependent loads of a phase from the winning record (block wb): lane
 // s < n reads the history pair at planes h0 + 2s, h0 + 2s + 1, and every lane
 // reads NE wave-uniform pairs at planes e0 + 2x.  One pass re-reads until every
 // granule carries the record's tag.  Returns false on timeout.
-template <int NE, bool SYS = false>
-__device__ __forceinline__ bool load_extras(const gu64* rec, int rs, int wb, int h0, int n, int e0,
+template <int NE, bool SYS = false, int rs = CHAIN_MAX_BLOCKS>
+__device__ __forceinline__ bool load_extras(const gu64* rec, int wb, int h0, int n, int e0,
                                             unsigned tag, double& hv, double (&ev)[2],
                                             State* st) {
   const int lane = threadIdx.x & 63;
@@ -357,8 +357,8 @@ __device__ __forceinline__ bool load_extras(const gu64* rec, int rs, int wb, int
 // keys (every lane the same winner), its lanes store the winner's extras, then
 // lane 0 the header (program order: the extras leave first).  RATIO: header v,
 // row, t; extras [extra, history].
-template <int NW, bool RATIO, bool SYS = false, typename Dst, typename Hist>
-__device__ __forceinline__ void publish_record(Dst dst, int nd, int rs, unsigned tag, int nh,
+template <int NW, bool RATIO, bool SYS = false, int rs = CHAIN_MAX_BLOCKS, typename Dst, typename Hist>
+__device__ __forceinline__ void publish_record(Dst dst, int nd, unsigned tag, int nh,
                                                const KeyP (&sk)[NW], Hist hist,
                                                unsigned stopbit = 0u) {
   const int lane = threadIdx.x & 63;
@@ -413,6 +413,55 @@ __device__ __forceinline__ void publish_record(Dst dst, int nd, int rs, unsigned
   }
 }
 
+// The single-GPU form of publish_record: one destination, no stop bit.  (The
+// shard form's destination loop and stop bit, compiled out for one
+// destination, still measured 0.1-0.3 us per pivot slower inside chain_kernel:
+// profiles/r03/ab_chain_regression_bisect.jsonl.)
+template <int NW, bool RATIO, typename Hist>
+__device__ __forceinline__ void publish_local(gu64* rec, int b, unsigned tag, int nh,
+                                              const KeyP (&sk)[NW], Hist hist) {
+  const int lane = threadIdx.x & 63;
+  KeyP k;
+  if constexpr (NW == 4) {
+    // one LDS read (lane x < 4 takes wave x's key) and two quad DPP steps,
+    // instead of four dependent broadcast reads and compares
+    k = lane < NW ? sk[lane] : keyp_none();
+    kmin2_dpp<0xB1>(k);  // quad_perm [1,0,3,2]
+    kmin2_dpp<0x4E>(k);  // quad_perm [2,3,0,1]
+    k = key_of_lane(k, 0);
+  } else {
+    k = sk[0];
+#pragma unroll
+    for (int x = 1; x < NW; ++x) kmin2(k, sk[x].v, sk[x].t, sk[x].row, sk[x].a, sk[x].b);
+  }
+  const int ww = (int)k.b;  // the winning wave (a payload slot of the block key)
+  const bool none = k.row < 0;
+  gu64* rb = rec + b;
+  constexpr int H0 = RATIO ? RATIO_HDR + 2 : ENTER_HDR;  // first history plane
+  if (!none) {
+    // lane x < 2*nh: history granule x; RATIO: lanes 62, 63 the extra (row's RHS)
+    if (lane < 2 * nh) {
+      const unsigned long long x =
+          (unsigned long long)__double_as_longlong(hist(ww, k.row, lane >> 1));
+      g_store(rb + (size_t)(H0 + lane) * CHAIN_MAX_BLOCKS, tag,
+              (lane & 1) ? (unsigned)(x >> 32) : (unsigned)x);
+    }
+    if (RATIO && lane >= 62) {
+      const unsigned long long x =
+          (unsigned long long)__double_as_longlong(hist(ww, k.row, 33));
+      g_store(rb + (size_t)(RATIO_HDR + (lane - 62)) * CHAIN_MAX_BLOCKS, tag,
+              (lane & 1) ? (unsigned)(x >> 32) : (unsigned)x);
+    }
+  }
+  if (lane == 0) {
+    const unsigned long long vb = (unsigned long long)__double_as_longlong(RATIO ? k.v : k.a);
+    g_store(rb + 0 * CHAIN_MAX_BLOCKS, tag, (unsigned)vb);
+    g_store(rb + 1 * CHAIN_MAX_BLOCKS, tag, (unsigned)(vb >> 32));
+    g_store(rb + 2 * CHAIN_MAX_BLOCKS, tag, none ? 0xffffffffu : (unsigned)k.row);
+    if (RATIO) g_store(rb + 3 * CHAIN_MAX_BLOCKS, tag, none ? 0xffffffffu : (unsigned)k.t);
+  }
+}
+
 // system-scope load of one double (the sharded chain's row gather from a peer)
 __device__ __forceinline__ double sys_load(const double* p) {
   return __longlong_as_double((long long)__hip_atomic_load(
@@ -420,29 +469,535 @@ __device__ __forceinline__ double sys_load(const double* p) {
 }
 
 // ---------------------------------------------------------------------------
-// chain_kernel<KMAX, CB, SH>: the pivots of one window (npiv <= KMAX slots).
-// SH = false: single GPU (row0 = 0).  SH = true: this rank's row block of a
-// row-sharded tableau: the columns, objective row and entering
-// exchange are replicated per rank (every rank computes the same values), the
-// ratio exchange is global (every block's record goes to every rank's
-// buffer, polled locally), and the leaving row's stale values are gathered
-// from the owner's tableau through a peer pointer.  grid = B blocks of CB threads (one block per CU,
-// every block resident); block b owns columns [b*cpb, ...) and rows
-// [b*rpb, ...), cpb, rpb <= CB, one of each per thread.  Wave 0 of a block
-// polls the record headers and hands the winner to the block through LDS;
-// every thread then loads what its column / row needs (the winning record's
-// history beside the stale tableau value).  n_ep / enter_part: pivot 0's
-// entering partials, written by the previous kernel (norm<INIT> or the
-// previous window's chain); the chain writes one partial per block there for
-// the next window.
+// chain_kernel<KMAX, CB>: the pivots of one window (npiv <= KMAX slots) on one
+// GPU.  grid = B blocks of CB threads (one block per CU, every block
+// resident); block b owns columns [b*cpb, ...) and rows [b*rpb, ...),
+// cpb, rpb <= CB, one of each per thread.  Wave 0 of a block polls the record
+// headers and hands the winner to the block through LDS; every thread then
+// loads what its column / row needs (the winning record's history beside the
+// stale tableau value).  n_ep / enter_part: pivot 0's entering partials,
+// written by the previous kernel (norm<INIT> or the previous window's chain);
+// the chain writes one partial per block there for the next window.
 // ---------------------------------------------------------------------------
-template <int KMAX, int CB, bool SH = false>
+template <int KMAX, int CB>
 __global__ __launch_bounds__(CB) void chain_kernel(
     Key* __restrict__ enter_part, State* st, const Params* __restrict__ prm, int n_ep,
     const double* __restrict__ A, int64_t ld, int64_t m, int64_t N, double* __restrict__ obj,
     Window win, int npiv, int64_t* __restrict__ basis, int64_t* __restrict__ hist,
     unsigned long long* gr_enter_, unsigned long long* gr_ratio_, int cpb, int rpb,
-    const ChainPeers* __restrict__ pep) {
+    const ChainPeers* __restrict__ /*pe: shards only*/) {
+  static_assert(KMAX <= 32, "slots are lane-indexed and fit the window buffers");
+  constexpr int NW = CB / 64;
+  constexpr int CH = KMAX % 8 == 0 ? 8 : KMAX % 4 == 0 ? 4 : 2;
+  // LH: the window histories f_s[i] (rows) and p_s[j] (columns) live in LDS,
+  // slot-major, one column per thread: a phase reads its thread's slots once
+  // and appends one, instead of a 2*KMAX-select register update on the path
+  // to the record (and the winner's history is published straight from them)
+  constexpr bool LH = KMAX * CB * 16 <= 128 * 1024;
+  __shared__ double fsl[LH ? KMAX : 1][LH ? CB : 1];
+  __shared__ double psl[LH ? KMAX : 1][LH ? CB : 1];
+  __shared__ double hl33[NW];  // LH: the wave winners' RHS (the ratio record's extra)
+  // one block per CU: the record protocol is validated for that residency
+  // (with LH the histories already take most of it)
+  constexpr int PIN = LH ? (82 * 1024 - KMAX * CB * 16 > 8 ? (82 * 1024 - KMAX * CB * 16) / 8 : 1)
+                         : 80 * 128;
+  __shared__ double lds_pin[PIN];
+  __shared__ int64_t bc_idx;  // the winner handed from wave 0 to the block
+  __shared__ double bc_val;
+  __shared__ int bc_blk;
+  __shared__ KeyP sk[NW];       // the waves' best keys (payload b = wave index)
+  __shared__ double hl[LH ? 1 : NW][34];  // their winners' histories (+ [33]: the row's RHS)
+  gu64* gr_enter = (gu64*)gr_enter_;
+  gu64* gr_ratio = (gu64*)gr_ratio_;
+  const int B = gridDim.x;
+  const int b = blockIdx.x;
+  const int t = threadIdx.x;
+  const int lane = t & 63;
+  const int w = t >> 6;
+  const bool w0 = t < 64;
+  const bool leader = b == 0 && t == 0;
+  // --- everything that does not depend on a pivot, in one batch ---
+  const int32_t status0 = st->status;
+  const int64_t forced_c = st->forced_c;
+  const int64_t forced_r = st->forced_r;
+  const int64_t it0 = st->iters;
+  const int64_t hist_cap = st->hist_cap;
+  const uint32_t E = *win.epoch;
+  const int32_t rule = prm->rule;
+  const double eps_piv = prm->eps_piv;
+  const double eps_opt = prm->eps_opt;
+  const int64_t n_enter = prm->n_enter;
+  const int64_t iter_limit = prm->iter_limit;
+  const bool skip = prm->skip_zero != 0;
+  const uint32_t W = (E + 1u) & TAG_EPOCH;  // this window's epoch
+  // my column and my row
+  const int64_t j = (int64_t)b * cpb + t;
+  const bool jlive = t < cpb && j < N;
+  const int64_t jc = jlive ? j : 0;
+  // rows sit on waves 1.. when they fit (roff = 64), so the polling wave 0
+  // issues no row-side stores (f_q) that its next poll's vmcnt wait would
+  // also have to drain; the pivot bookkeeping is stored by the last thread
+  const int roff = rpb <= CB - 64 ? 64 : 0;
+  const int64_t i = (int64_t)b * rpb + (t - roff);
+  const bool ilive = t >= roff && t - roff < rpb && i < m;
+  const int64_t ic = ilive ? i : 0;
+  double o = obj[jc];
+  uint32_t tg = jlive ? win.tag[jc] : 0u;
+  const uint32_t tg0 = tg;
+  // The RHS column N-1 is never an entering candidate and its pivot-row value
+  // is the ratio record's p_q[rhs] (the row owner's current RHS / pivot), so
+  // when the host sizes the grid by the N-1 candidate columns (B * cpb == N-1:
+  // 64 blocks at config 3, a single-pass poll) the last thread of the last
+  // block keeps it beside its own column: objective value, tag, p history.
+  const bool xown = (int64_t)B * cpb == N - 1 && b == B - 1 && t == CB - 1;
+  double ox = xown ? obj[N - 1] : 0.0;
+  uint32_t tgx = xown ? win.tag[N - 1] : 0u;
+  const uint32_t tgx0 = tgx;
+  uint32_t zmx = 0u;
+  __shared__ double pxl[KMAX];  // p_s[N-1] (xown only)
+  double bcur = A[(N - 1) * ld + ic];   // current RHS of my row (stale + applied slots)
+  int64_t bas = basis[ic];              // basis[i] (Bland's tie key)
+  double fs[KMAX], ps[KMAX];            // f_s[i], p_s[j] of this window
+#pragma unroll
+  for (int s = 0; s < KMAX; ++s) fs[s] = ps[s] = 0.0;
+  int64_t slot_r = 0, slot_c = -1;      // lane s: (r_s, c_s)
+  // per-thread slot masks (bit s): my row left at slot s (i == r_s), my column
+  // entered at slot s (j == c_s), p_s[j] == 0 under the skip rule
+  uint32_t rmask = 0u, cmask = 0u, zmask = 0u;
+  if (t == 0) lds_pin[b % PIN] = 0.0;
+  if (status0 != ST_RUNNING) {          // grid-uniform: no pivot in this window
+    if (leader)
+      for (int s = 0; s < npiv; ++s) win.made[s] = 0;  // (the flush counts made slots)
+    return;
+  }
+  if (leader) {
+    // the flush's record counter; reset write-through and drained before this
+    // block's first record (every other block adds to it only after polling
+    // that record)
+    __hip_atomic_store((gu32*)win.nlist, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  int q = 0;
+  int64_t r_prev = -1;
+  double f_prev = 0.0, prhs = 0.0;  // my f_{q-1}[i]; p_{q-1}[rhs] = RHS of r_{q-1} / pivot
+  int32_t stop_status = ST_RUNNING;
+  for (; q < npiv; ++q) {
+    // ================= ratio phase q =================
+    SPX_PROBE(q, 0, 0, true);
+    int64_t c;
+    double zc;
+    int wb = 0;
+    if (q == 0) {
+      // entering partials of the previous kernel (visible: kernel boundary)
+      Keys8 kk;
+      keys_issue(kk, enter_part, n_ep);
+      KeyR e = keys_reduce(kk, enter_part, n_ep);
+      wave_min_dpp(e);
+      c = e.row;
+      zc = c >= 0 ? obj[c] : 0.0;
+    } else {
+      if (w0) {
+        KeyP e;
+        const bool ok =
+            poll_records<false, 3>(gr_enter, B, rec_tag(W, q - 1, GK_ENTER), rule, e, st);
+        if (t == 0) {
+          bc_idx = ok ? e.row : -2;
+          bc_val = e.a;
+          bc_blk = (int)e.b;
+        }
+        SPX_PROBE_CHAIN(q - 1, 3);
+      }
+      __syncthreads();
+      c = bc_idx;
+      zc = bc_val;
+      wb = bc_blk;
+      if (c == -2) return;  // a wait timed out (ST_FAULT stored)
+    }
+    SPX_PROBE(q, 0, 1, true);
+    if (forced_c >= 0) {
+      c = forced_c;
+      zc = obj[c];  // (forced pivots are single-pivot windows: q == 0)
+    }
+    const int64_t it = it0 + q;
+    if (c < 0) stop_status = ST_OPTIMAL;
+    else if (forced_r < 0 && it >= iter_limit) stop_status = ST_LIMIT;
+    if (stop_status != ST_RUNNING) break;  // grid-uniform
+    // column c on my row: stale + pending slots, in slot order; p_s[c] (lane
+    // s) from the winning entering record's history
+    double fv = A[c * ld + ic];
+    if constexpr (LH) {  // my row's f history, read while the gathers are in flight
+#pragma unroll
+      for (int s = 0; s < KMAX; ++s) fs[s] = fsl[s][t];
+    }
+    double pcl = 0.0, unused[2];
+    if (q > 0 &&
+        !load_extras<0>(gr_enter, wb, ENTER_HDR, q, 0, rec_tag(W, q - 1, GK_ENTER), pcl, unused,
+                        st))
+      return;
+    SPX_PROBE(q, 2, 0, fv != 12345.678 && pcl != 12345.678);  // loads arrived
+    // RHS: apply slot q-1 (the slots before it are already in bcur)
+    if (q > 0) bcur = apply_sel(bcur, i == r_prev, false, true, f_prev, prhs, skip);
+    // apply_sel's special cases as masks: column c entered earlier in this
+    // window or p_s[c] == 0 under the skip rule (uniform: the exact loop), my
+    // row left at slot s (rmask: p_s[c] replaces the msub on that lane).
+    // Otherwise a slot is one msub (~5 VALU ops instead of ~25).
+    const uint32_t qm = (1u << q) - 1u;
+    if (__ballot(lane < q && (slot_c == c || (skip && pcl == 0.0))) == 0ull) {
+      if (__ballot((rmask & qm) != 0u) == 0ull) {
+#pragma unroll
+        for (int c8 = 0; c8 < KMAX; c8 += CH) {
+          if (c8 < q) {
+#pragma unroll
+            for (int u = 0; u < CH; ++u) {
+              const int s = c8 + u;
+              const double x = msub(fv, fs[s], rdlane(pcl, s));
+              fv = s < q ? x : fv;
+            }
+          }
+        }
+      } else {
+#pragma unroll
+        for (int c8 = 0; c8 < KMAX; c8 += CH) {
+          if (c8 < q) {
+#pragma unroll
+            for (int u = 0; u < CH; ++u) {
+              const int s = c8 + u;
+              const double p_s = rdlane(pcl, s);
+              double x = msub(fv, fs[s], p_s);
+              x = ((rmask >> s) & 1u) ? p_s : x;
+              fv = s < q ? x : fv;
+            }
+          }
+        }
+      }
+    } else {
+#pragma unroll
+      for (int c8 = 0; c8 < KMAX; c8 += CH) {
+        if (c8 < q) {
+#pragma unroll
+          for (int u = 0; u < CH; ++u) {
+            const int s = c8 + u;
+            const bool act = s < q;
+            const bool isr = i == rdlane64(slot_r, s);
+            const bool isc = c == rdlane64(slot_c, s);
+            fv = apply_sel(fv, isr, isc, act, fs[s], rdlane(pcl, s), skip);
+          }
+        }
+      }
+    }
+    SPX_PROBE(q, 2, 1, fv != 12345.678);  // slots applied
+    if constexpr (LH) {
+      fsl[q][t] = fv;
+    } else {
+#pragma unroll
+      for (int s = 0; s < KMAX; ++s) fs[s] = (s == q) ? fv : fs[s];
+    }
+    f_prev = fv;
+    KeyP k = keyp_none();
+    if (ilive) {
+      if (forced_r >= 0) {
+        if (i == forced_r) kmin2(k, 0.0, 0, i, 0.0, 0.0);
+      } else if (fv > eps_piv) {
+        const double rq = bcur / fv;
+        if (rq == rq) kmin2(k, rq, rule == RULE_BLAND ? bas : i, i, 0.0, 0.0);
+      }
+    }
+    SPX_PROBE(q, 0, 2, fv != 12345.678);
+    // publish: the wave winner puts its f history and RHS in LDS, the block's
+    // winner is published by wave 0 (rows grow with the lane: Dantzig's tie key)
+    k = key_of_lane(k, wave_argmin(k.v, k.t, k.row >= 0, rule != RULE_BLAND));
+    if (ilive && k.row == i) {
+      if constexpr (LH) {
+        hl33[w] = bcur;
+      } else {
+#pragma unroll
+        for (int s = 0; s < KMAX; ++s)
+          if (s <= q) hl[w][s] = fs[s];
+        hl[w][33] = bcur;
+      }
+    }
+    if (lane == 0) sk[w] = KeyP{k.v, k.t, k.row, 0.0, (double)w};
+    SPX_PROBE(q, 2, 2, k.v != 12345.678);  // wave argmin + LDS hand-off issued
+    __syncthreads();
+    SPX_PROBE(q, 2, 3, true);              // every wave of the block arrived
+    if (w0) {
+      publish_local<NW, true>(gr_ratio, b, rec_tag(W, q, GK_RATIO), q + 1, sk,
+                               [&](int ww, int64_t row, int x) -> double {
+                                 if constexpr (LH)
+                                   return x == 33 ? hl33[ww]
+                                                  : fsl[x][(int)(row - (int64_t)b * rpb) + roff];
+                                 else
+                                   return hl[ww][x];
+                               });
+      SPX_PROBE_CHAIN(q, 0);
+    }
+    // f_q for the flush / row_fix (later kernels): stored after the record, so
+    // these stores never queue in front of it
+    if (ilive) win.F[(int64_t)q * ld + i] = fv;
+    SPX_PROBE(q, 0, 3, true);
+    // ================= norm phase q =================
+    SPX_PROBE(q, 1, 0, true);
+    if (w0) {
+      KeyP rk;
+      const unsigned rtag = rec_tag(W, q, GK_RATIO);
+      const bool ok = rule == RULE_BLAND
+                          ? poll_records<true, 4>(gr_ratio, B, rtag, rule, rk, st)
+                          : poll_records<true, 3>(gr_ratio, B, rtag, rule, rk, st);
+      if (t == 0) {
+        bc_idx = ok ? rk.row : -2;
+        bc_blk = (int)rk.b;
+      }
+      SPX_PROBE_CHAIN(q, 1);
+    }
+    __syncthreads();
+    const int64_t r = bc_idx;
+    wb = bc_blk;
+    if (r == -2) return;
+    SPX_PROBE(q, 1, 1, true);
+    if (q == 0 && leader) *win.epoch = W;  // every block has read E (its record carries W)
+    if (r < 0) {
+      stop_status = ST_UNBOUNDED;
+      break;
+    }
+    // row r on my column: stale + pending slots.  f_s[r] (lane s <= q, lane q
+    // the pivot element) and the row's RHS from the winning ratio record
+    double v = A[jc * ld + r];
+    if constexpr (LH) {  // my column's p history, read while the gathers are in flight
+#pragma unroll
+      for (int s = 0; s < KMAX; ++s) ps[s] = psl[s][t];
+    }
+    double frl = 0.0, ex[2];
+    if (!load_extras<1>(gr_ratio, wb, RATIO_HDR + 2, q + 1, RATIO_HDR, rec_tag(W, q, GK_RATIO),
+                        frl, ex, st))
+      return;
+    SPX_PROBE(q, 3, 0, v != 12345.678 && frl != 12345.678);  // loads arrived
+    const double piv = rdlane(frl, q);
+    prhs = ex[0] / piv;  // p_q[rhs]: lazy_norm's p = v / piv of the RHS column
+    // Special cases as masks: row r left earlier in the window (uniform: the
+    // exact loop), my column entered at slot s (cmask: the value becomes 0),
+    // p_s[j] == 0 under the skip rule (zmask: the value is kept)
+    const uint32_t qmn = (1u << q) - 1u;
+    const bool zb = (zmask & qmn) != 0u;
+    if (__ballot(lane < q && slot_r == r) == 0ull) {
+      if (__ballot(jlive && ((zmask | cmask) & qmn) != 0u) == 0ull) {
+#pragma unroll
+        for (int c8 = 0; c8 < KMAX; c8 += CH) {
+          if (c8 < q) {
+#pragma unroll
+            for (int u = 0; u < CH; ++u) {
+              const int s = c8 + u;
+              const double x = msub(v, rdlane(frl, s), ps[s]);
+              v = s < q ? x : v;
+            }
+          }
+        }
+      } else {
+#pragma unroll
+        for (int c8 = 0; c8 < KMAX; c8 += CH) {
+          if (c8 < q) {
+#pragma unroll
+            for (int u = 0; u < CH; ++u) {
+              const int s = c8 + u;
+              double x = msub(v, rdlane(frl, s), ps[s]);
+              x = ((zmask >> s) & 1u) ? v : x;
+              x = ((cmask >> s) & 1u) ? 0.0 : x;
+              v = s < q ? x : v;
+            }
+          }
+        }
+      }
+    } else {
+#pragma unroll
+      for (int c8 = 0; c8 < KMAX; c8 += CH) {
+        if (c8 < q) {
+#pragma unroll
+          for (int u = 0; u < CH; ++u) {
+            const int s = c8 + u;
+            const bool act = s < q;
+            const bool isr = r == rdlane64(slot_r, s);
+            const bool isc = jc == rdlane64(slot_c, s);
+            v = apply_sel(v, isr, isc, act, rdlane(frl, s), ps[s], skip);
+          }
+        }
+      }
+    }
+    SPX_PROBE(q, 3, 1, v != 12345.678);  // slots applied
+    KeyP ek = keyp_none();
+    double pq = 0.0;  // p_q[j]
+    if (jlive) {
+      const double p = v / piv;
+      pq = p;
+      zmask |= (skip && p == 0.0) ? (1u << q) : 0u;
+      cmask |= (j == c) ? (1u << q) : 0u;
+      if constexpr (!LH) {
+#pragma unroll
+        for (int s = 0; s < KMAX; ++s) ps[s] = (s == q) ? p : ps[s];
+      }
+      const bool nz = (p != 0.0) || !skip;
+      if (j == c) {
+        o = 0.0;
+      } else if (nz) {
+        o = msub(o, zc, p);
+      }
+      const bool tagged = (tg & TAG_EPOCH) == W;
+      if (nz) {
+        tg = W | ((j == c || (tagged && (tg & TAG_SPECIAL))) ? TAG_SPECIAL : 0u) |
+             (zb ? TAG_ZERO : 0u);
+      } else if (tagged) {
+        tg = tg | TAG_ZERO;
+      }
+      // key (o, j) under Dantzig, (0, j) under Bland; payload o (z_c)
+      if (j < n_enter && o < -eps_opt) kmin2(ek, rule == RULE_BLAND ? 0.0 : o, j, j, o, 0.0);
+    }
+    if (xown) {  // the RHS column: the same update with p = p_q[rhs] (never j == c)
+      const bool zbx = (zmx & qmn) != 0u;
+      zmx |= (skip && prhs == 0.0) ? (1u << q) : 0u;
+      const bool nz = (prhs != 0.0) || !skip;
+      if (nz) ox = msub(ox, zc, prhs);
+      const bool tagged = (tgx & TAG_EPOCH) == W;
+      if (nz) {
+        tgx = W | ((tagged && (tgx & TAG_SPECIAL)) ? TAG_SPECIAL : 0u) | (zbx ? TAG_ZERO : 0u);
+      } else if (tagged) {
+        tgx = tgx | TAG_ZERO;
+      }
+      pxl[q] = prhs;
+    }
+    if (ilive && i == r) bas = c;
+    rmask |= (i == r) ? (1u << q) : 0u;
+    if (lane == q) {
+      slot_r = r;
+      slot_c = c;
+    }
+    r_prev = r;
+    SPX_PROBE(q, 1, 2, v != 12345.678);
+    ek = key_of_lane(ek, wave_argmin(ek.v, ek.t, ek.row >= 0, true));  // columns grow with the lane
+    if constexpr (LH) {
+      psl[q][t] = pq;
+    } else if (q + 1 < npiv && jlive && ek.row == j) {
+#pragma unroll
+      for (int s = 0; s < KMAX; ++s)
+        if (s <= q) hl[w][s] = ps[s];
+    }
+    if (lane == 0) sk[w] = KeyP{ek.v, ek.t, ek.row, ek.a, (double)w};
+    SPX_PROBE(q, 3, 2, ek.v != 12345.678);  // wave argmin + LDS hand-off issued
+    __syncthreads();
+    SPX_PROBE(q, 3, 3, true);               // every wave of the block arrived
+    if (w0) {
+      if (q + 1 < npiv) {
+        publish_local<NW, false>(gr_enter, b, rec_tag(W, q, GK_ENTER), q + 1, sk,
+                                  [&](int ww, int64_t col, int x) -> double {
+                                    if constexpr (LH)
+                                      return psl[x][(int)(col - (int64_t)b * cpb)];
+                                    else
+                                      return hl[ww][x];
+                                  });
+      } else if (t == 0) {
+        // the next window's pivot-0 partial (read after the kernel boundary)
+        KeyP kb = sk[0];
+#pragma unroll
+        for (int x = 1; x < NW; ++x) kmin2(kb, sk[x].v, sk[x].t, sk[x].row, sk[x].a, sk[x].b);
+        store_key(enter_part + b, KeyR{kb.v, kb.t, kb.row});
+        // the next window reduces n_ep partials (norm<INIT>'s per-WG count can
+        // exceed B, e.g. 512-thread blocks): the ones past this grid's must not
+        // keep an earlier kernel's keys
+        for (int x = b + B; x < n_ep; x += B) store_key(enter_part + x, keyr_none());
+      }
+      SPX_PROBE_CHAIN(q, 2);
+    }
+    // stores for later kernels, after the record (never queued in front of it):
+    // the pivot's bookkeeping (the flush and row_fix read p from the records)
+    if (b == 0 && t == CB - 1) {  // block 0's last thread: not in the polling wave
+      st->r = r;
+      st->c = c;
+      st->zc = zc;
+      st->piv = piv;
+      win.r[q] = r;
+      win.c[q] = c;
+      win.made[q] = 1;
+      basis[r] = c;
+      if (it < hist_cap) {
+        hist[2 * it] = r;
+        hist[2 * it + 1] = c;
+      }
+    }
+
+    SPX_PROBE(q, 1, 3, true);
+  }
+  // ---- the window ends after slot q (q pivots made) ----
+  if (stop_status != ST_RUNNING && leader) {
+    st->status = stop_status;
+    if (stop_status == ST_OPTIMAL) st->c_next = -1;
+    for (int s = q; s < npiv; ++s) win.made[s] = 0;
+  }
+  if (jlive) {
+    obj[j] = o;
+    if (tg != tg0) win.tag[j] = tg;
+  }
+  if (xown) {
+    obj[N - 1] = ox;
+    if (tgx != tgx0) win.tag[N - 1] = tgx;
+  }
+  if (q == 0) return;  // no pivot made: nothing to compact (the flush sees nm == 0)
+  // compact the window's touched columns into records for the flush (as
+  // lazy_norm's last slot): wave ballot + LDS prefix + one atomic per block;
+  // the RHS column (xown) follows its wave's own columns
+  const bool mine = jlive && (tg & TAG_EPOCH) == W;
+  const bool minex = xown && (tgx & TAG_EPOCH) == W;
+  __shared__ int wcnt[NW];
+  __shared__ int base;
+  const uint64_t bal = __ballot(mine);
+  const uint64_t balx = __ballot(minex);
+  if (lane == 0) wcnt[w] = __popcll(bal) + __popcll(balx);
+  __syncthreads();
+  if (t == 0) {
+    int tot = 0;
+    for (int x = 0; x < NW; ++x) tot += wcnt[x];
+    base = tot ? (int)__hip_atomic_fetch_add((gu32*)win.nlist, (unsigned)tot, __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT)
+               : 0;
+  }
+  __syncthreads();
+  int pos = base + __popcll(bal & ((1ull << lane) - 1ull));
+  for (int x = 0; x < w; ++x) pos += wcnt[x];
+  if (mine && pos < N) {
+    double* rc_ = win.rec + (int64_t)pos * RECW;
+    reinterpret_cast<int64_t*>(rc_)[0] = j | ((int64_t)(tg >> 30) << 32);
+#pragma unroll
+    for (int s = 0; s < KMAX; ++s)
+      if (s < q) rc_[2 + s] = LH ? psl[s][t] : ps[s];
+  }
+  if (minex) {
+    const int px = pos - __popcll(bal & ((1ull << lane) - 1ull)) + __popcll(bal);
+    if (px < N) {
+      double* rc_ = win.rec + (int64_t)px * RECW;
+      reinterpret_cast<int64_t*>(rc_)[0] = (N - 1) | ((int64_t)(tgx >> 30) << 32);
+#pragma unroll
+      for (int s = 0; s < KMAX; ++s)
+        if (s < q) rc_[2 + s] = pxl[s];
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// chain_shard_kernel<KMAX, CB>: chain_kernel for this rank's row block of a
+// row-sharded tableau.  The columns, objective row and entering
+// exchange are replicated per rank (every rank computes the same values), the
+// ratio exchange is global (every block's record goes to every rank's buffer,
+// polled locally), and the leaving row's stale values are gathered from the
+// owner's tableau through a peer pointer.  Rows are local (i), records, slots
+// and the basis speak global rows (ig = row0 + i).  pe: the peers' table, in
+// device memory (a by-value kernel argument of its size measurably slowed the
+// chain).  The single-GPU chain_kernel is this kernel with one rank, kept as
+// its own body: folded into this one it measured ~1 us per pivot slower
+// (register allocation of a 254-VGPR kernel; profiles/r03/ab_chain_*.jsonl).
+// ---------------------------------------------------------------------------
+template <int KMAX, int CB>
+__global__ __launch_bounds__(CB) void chain_shard_kernel(
+    Key* __restrict__ enter_part, State* st, const Params* __restrict__ prm, int n_ep,
+    const double* __restrict__ A, int64_t ld, int64_t m, int64_t N, double* __restrict__ obj,
+    Window win, int npiv, int64_t* __restrict__ basis, int64_t* __restrict__ hist,
+    unsigned long long* gr_enter_, unsigned long long* gr_ratio_, int cpb, int rpb,
+    const ChainPeers* __restrict__ pe) {
   static_assert(KMAX <= 32, "slots are lane-indexed and fit the window buffers");
   constexpr int NW = CB / 64;
   constexpr int CH = KMAX % 8 == 0 ? 8 : KMAX % 4 == 0 ? 4 : 2;
@@ -487,33 +1042,28 @@ __global__ __launch_bounds__(CB) void chain_kernel(
   const int64_t iter_limit = prm->iter_limit;
   const bool skip = prm->skip_zero != 0;
   const uint32_t W = (E + 1u) & TAG_EPOCH;  // this window's epoch (the same on every rank)
-  // SH: the peers' table lives in device memory (a by-value kernel argument of
-  // this size measurably slowed the single-GPU chain); unused otherwise
-  const ChainPeers* pe = pep;
-  // row shards: my rank's rows start at row0; the ratio records of all nr * B
-  // blocks are polled (block slot rank * B + b, planes RS apart)
-  const int rank = SH ? pe->rank : 0;
-  const int nr = SH ? pe->nranks : 1;
-  const int64_t row0 = SH ? pe->row0[rank] : 0;
-  constexpr int RS = SH ? CHAIN_SH_SLOTS : CHAIN_MAX_BLOCKS;
-  const int BR = SH ? nr * B : B;
-  const int bs = SH ? rank * B + b : b;
+  // my rank's rows start at row0; the ratio records of all nr * B blocks are
+  // polled (block slot rank * B + b, planes RS apart)
+  const int rank = pe->rank;
+  const int nr = pe->nranks;
+  const int64_t row0 = pe->row0[rank];
+  constexpr int RS = CHAIN_SH_SLOTS;
+  const int BR = nr * B;
+  const int bs = rank * B + b;
   // rank 0's time-limit stop request rides in its ratio records (bit 31 of
   // granule 3); read once per window, so every rank stops at the window's start
   const unsigned stopbit =
-      (SH && rank == 0 && pe->stop_req &&
+      (rank == 0 && pe->stop_req &&
        __hip_atomic_load(const_cast<int32_t*>(pe->stop_req), __ATOMIC_RELAXED,
                          __HIP_MEMORY_SCOPE_SYSTEM) != 0)
           ? 1u : 0u;
-  // the ratio buffer of pivot it0 + q: SH alternates two halves by pivot
-  // parity (a rank's entering exchange is local, so it may publish ratio
-  // q + 1 before a peer has read ratio q; never q + 2)
+  // the ratio buffer of pivot it0 + q: two halves by pivot parity (a rank's
+  // entering exchange is local, so it may publish ratio q + 1 before a peer
+  // has read ratio q; never q + 2)
   auto ratio_buf = [&](int d, int qq) -> gu64* {
-    if constexpr (SH)
-      return (gu64*)pe->ratio[d] + (size_t)((it0 + qq) & 1) * RATIO_REC * RS;
-    else
-      return gr_ratio;
+    return (gu64*)pe->ratio[d] + (size_t)((it0 + qq) & 1) * RATIO_REC * RS;
   };
+  (void)gr_ratio;
   // my column and my row
   const int64_t j = (int64_t)b * cpb + t;
   const bool jlive = t < cpb && j < N;
@@ -583,9 +1133,8 @@ __global__ __launch_bounds__(CB) void chain_kernel(
     } else {
       if (w0) {
         KeyP e;
-        const bool ok =
-            poll_records<false, 3>(gr_enter, B, CHAIN_MAX_BLOCKS, rec_tag(W, q - 1, GK_ENTER),
-                                   rule, e, st);
+        const bool ok = poll_records<false, 3>(gr_enter, B,
+                                               rec_tag(W, q - 1, GK_ENTER), rule, e, st);
         if (t == 0) {
           bc_idx = ok ? e.row : -2;
           bc_val = e.a;
@@ -617,7 +1166,7 @@ __global__ __launch_bounds__(CB) void chain_kernel(
     }
     double pcl = 0.0, unused[2];
     if (q > 0 &&
-        !load_extras<0>(gr_enter, CHAIN_MAX_BLOCKS, wb, ENTER_HDR, q, 0,
+        !load_extras<0>(gr_enter, wb, ENTER_HDR, q, 0,
                         rec_tag(W, q - 1, GK_ENTER), pcl, unused, st))
       return;
     SPX_PROBE(q, 2, 0, fv != 12345.678 && pcl != 12345.678);  // loads arrived
@@ -707,7 +1256,7 @@ __global__ __launch_bounds__(CB) void chain_kernel(
     __syncthreads();
     SPX_PROBE(q, 2, 3, true);              // every wave of the block arrived
     if (w0) {
-      publish_record<NW, true, SH>([&](int d) { return ratio_buf(d, q) + bs; }, nr, RS,
+      publish_record<NW, true, true, RS>([&](int d) { return ratio_buf(d, q) + bs; }, nr,
                                    rec_tag(W, q, GK_RATIO), q + 1, sk,
                                    [&](int ww, int64_t row, int x) -> double {
                                      if constexpr (LH)
@@ -720,7 +1269,7 @@ __global__ __launch_bounds__(CB) void chain_kernel(
                                    stopbit);
       SPX_PROBE_CHAIN(q, 0);
     }
-    // f_q for the flush (a later kernel): stored after the record, so
+    // f_q for the flush / row_fix (later kernels): stored after the record, so
     // these stores never queue in front of it
     if (ilive) win.F[(int64_t)q * ld + i] = fv;
     SPX_PROBE(q, 0, 3, true);
@@ -731,9 +1280,7 @@ __global__ __launch_bounds__(CB) void chain_kernel(
       const unsigned rtag = rec_tag(W, q, GK_RATIO);
       bool stopq = false;
       const bool ok =
-          SH ? poll_records<true, 4, true>(ratio_buf(rank, q), BR, RS, rtag, rule, rk, st, &stopq)
-          : rule == RULE_BLAND ? poll_records<true, 4>(gr_ratio, B, RS, rtag, rule, rk, st)
-                               : poll_records<true, 3>(gr_ratio, B, RS, rtag, rule, rk, st);
+          poll_records<true, 4, true, RS>(ratio_buf(rank, q), BR, rtag, rule, rk, st, &stopq);
       if (t == 0) {
         bc_idx = ok ? (stopq ? -3 : rk.row) : -2;
         bc_blk = (int)rk.b;
@@ -746,7 +1293,7 @@ __global__ __launch_bounds__(CB) void chain_kernel(
     if (r == -2) return;
     SPX_PROBE(q, 1, 1, true);
     if (q == 0 && leader) *win.epoch = W;  // every block has read E (its record carries W)
-    if (r == -3) {  // (SH) rank 0's time-limit stop, seen by every rank at this pivot
+    if (r == -3) {  // rank 0's time-limit stop, seen by every rank at this pivot
       stop_status = ST_LIMIT;
       break;
     }
@@ -756,20 +1303,16 @@ __global__ __launch_bounds__(CB) void chain_kernel(
     }
     // row r on my column: stale + pending slots.  f_s[r] (lane s <= q, lane q
     // the pivot element) and the row's RHS from the winning ratio record
-    double v;
-    if constexpr (SH) {  // the owner's stale row (a peer's tableau unless it is mine)
-      const int own = wb / B;
-      if (own == rank) v = A[jc * ld + (r - row0)];
-      else v = sys_load(pe->A[own] + jc * pe->ld[own] + (r - pe->row0[own]));
-    } else {
-      v = A[jc * ld + r];
-    }
+    double v;  // the owner's stale row (a peer's tableau unless it is mine)
+    const int own = wb / B;
+    if (own == rank) v = A[jc * ld + (r - row0)];
+    else v = sys_load(pe->A[own] + jc * pe->ld[own] + (r - pe->row0[own]));
     if constexpr (LH) {  // my column's p history, read while the gathers are in flight
 #pragma unroll
       for (int s = 0; s < KMAX; ++s) ps[s] = psl[s][t];
     }
     double frl = 0.0, ex[2];
-    if (!load_extras<1, SH>(ratio_buf(rank, q), RS, wb, RATIO_HDR + 2, q + 1, RATIO_HDR,
+    if (!load_extras<1, true, RS>(ratio_buf(rank, q), wb, RATIO_HDR + 2, q + 1, RATIO_HDR,
                             rec_tag(W, q, GK_RATIO), frl, ex, st))
       return;
     SPX_PROBE(q, 3, 0, v != 12345.678 && frl != 12345.678);  // loads arrived
@@ -886,7 +1429,7 @@ __global__ __launch_bounds__(CB) void chain_kernel(
     SPX_PROBE(q, 3, 3, true);               // every wave of the block arrived
     if (w0) {
       if (q + 1 < npiv) {
-        publish_record<NW, false>([&](int) { return gr_enter + b; }, 1, CHAIN_MAX_BLOCKS,
+        publish_record<NW, false>([&](int) { return gr_enter + b; }, 1,
                                   rec_tag(W, q, GK_ENTER), q + 1, sk,
                                   [&](int ww, int64_t col, int x) -> double {
                                     if constexpr (LH)
@@ -908,7 +1451,7 @@ __global__ __launch_bounds__(CB) void chain_kernel(
       SPX_PROBE_CHAIN(q, 2);
     }
     // stores for later kernels, after the record (never queued in front of it):
-    // the pivot's bookkeeping (the flush reads p from the records)
+    // the pivot's bookkeeping (the flush and row_fix read p from the records)
     if (b == 0 && t == CB - 1) {  // block 0's last thread: not in the polling wave
       st->r = r;
       st->c = c;
@@ -923,11 +1466,10 @@ __global__ __launch_bounds__(CB) void chain_kernel(
         hist[2 * it + 1] = c;
       }
     }
-
     SPX_PROBE(q, 1, 3, true);
   }
-  if constexpr (SH) {
-    // Window-end barrier: a rank's next kernel (the flush) rewrites its
+  {
+    // Window-end barrier: a rank's next kernels (flush, row_fix) rewrite its
     // rows, so none may start while a peer still gathers one of them.  Every
     // block reports once its last row gather has returned (its values were
     // consumed before the last block barrier above); block 0 of every rank

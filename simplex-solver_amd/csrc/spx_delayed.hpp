@@ -741,7 +741,7 @@ __global__ __launch_bounds__(BLK) void flush_lds_kernel(double* __restrict__ A, 
     const int64_t j = hc & 0xffffffffll;
     if ((hc >> 32) == 0 && (PART || full)) {
       // fast path: the straight msub chain over the made slots, leaving rows
-      // included (the tail below rewrites those).  PART: the instance launched
+      // included (row_fix_kernel rewrites those).  PART: the instance launched
       // for a window of fewer than K pivots guards each slot (a separate
       // instance: the guards cost the full-window loop its register budget);
       // a full-size window that stopped early takes the exact path below
@@ -791,50 +791,64 @@ __global__ __launch_bounds__(BLK) void flush_lds_kernel(double* __restrict__ A, 
     hn = (k + D + 1 < cnt) ? hdr[rec_of(k + D + 1)] : 0;
   }
   wait_vmcnt<0>();  // no DMA may land in LDS after the wave has exited
-  // ---- the window's leaving rows in the fast-path columns (round 3; this was
-  // row_fix_kernel, a launch of its own) ----
-  // The fast path above ran the plain msub chain on every row, leaving rows
-  // included.  A fast-path column has no entering slot and every p_s[j] != 0,
-  // so a row r whose last leaving slot is Ls ends at p_Ls[j] followed by the
-  // msub updates of the slots after Ls (their leaving rows differ from r).
-  // The wave that stored this column's 128-row chunk rewrites those elements
-  // itself, behind its own stores (the vmcnt(0) above): nothing else writes
-  // them, so no hand-off is needed.  Lanes take the wave's records 64 at a time.
-  if (PART || full) {
-    uint32_t lm = 0u;  // slots whose row is in my 128 rows and leaves there last
-    for (int s = 0; s < nm; ++s) {
-      const int64_t rs = wr[s] - row0 - wrow;
-      if (rs < 0 || rs >= 128 || wrow + rs >= m_local) continue;
-      bool last = true;
-      for (int u = s + 1; u < nm; ++u) last &= wr[u] != wr[s];
-      if (last) lm |= 1u << s;
-    }
-    const double* __restrict__ vrec = win.rec;  // vector loads: one record per lane
-    while (lm != 0u) {
-      const int Ls = __builtin_ctz(lm);
-      lm &= lm - 1u;
-      const int rl = (int)(wr[Ls] - row0 - wrow);  // wave-uniform, 0..127
-      double fl[K];                                 // f_s[r] of the slots after Ls
-#pragma unroll
-      for (int s = 0; s < K; ++s) fl[s] = rdlane((rl & 1) ? f[s][1] : f[s][0], rl >> 1);
-      for (int k0 = 0; k0 < cnt; k0 += 64) {
-        const int kk = min(k0 + lane, cnt - 1);
-        const int64_t ro = rec_of(kk);
-        const int64_t h = reinterpret_cast<const int64_t*>(vrec)[ro];
-        double x = vrec[ro + 2 + Ls];
-#pragma unroll
-        for (int s = 0; s < K; ++s) {
-          const double y = msub(x, fl[s], vrec[ro + 2 + s]);
-          x = (s > Ls && s < nm) ? y : x;
-        }
-        if (k0 + lane < cnt && (h >> 32) == 0)
-          __builtin_nontemporal_store(x, A + (h & 0xffffffffll) * ld + wrow + rl);
-      }
-    }
-  }
   SPX_PROBE_WAVE(w, cnt);
   SPX_PROBE(K, 2, 1, true);
   SPX_PROBE_BLOCK(1);
+}
+
+// ---------------------------------------------------------------------------
+// row_fix_kernel<K>: after a window's flush (its made slots: a prefix of K),
+// rewrite the leaving rows of the fast-path columns (the window's records
+// without SPECIAL / ZERO flags; p values from the records).  For such a column no
+// pivot of the window enters it and every p_s[j] != 0, so a leaving row r
+// whose last leaving slot is L ends at p_L[j] followed by the later pivots'
+// msub updates (their leaving rows differ from r).  One thread per column.
+// ---------------------------------------------------------------------------
+template <int K>
+__global__ __launch_bounds__(BLK) void row_fix_kernel(double* __restrict__ A, int64_t ld,
+                                                      int64_t m_local, int64_t row0, int64_t N,
+                                                      Window win, int npiv) {
+  (void)N;
+  __shared__ double fr[K][K];  // fr[L][s] = f_s[r_L]
+  __shared__ int64_t rows[K];
+  __shared__ int lastL[K];
+  // one thread per record of the window (the flush's compacted list: column,
+  // path flags, p_0..p_{K-1}); all loads are independent: issue them together
+  const int kr = blockIdx.x * BLK + threadIdx.x;
+  const bool live = kr < *win.nlist;
+  const int64_t hdr = reinterpret_cast<const int64_t*>(win.rec)[(int64_t)(live ? kr : 0) * RECW];
+  const int64_t j = hdr & 0xffffffffll;
+  const bool fast = (hdr >> 32) == 0;  // not SPECIAL / ZERO: the flush's plain msub chain
+  int madeK = 0;  // made slots of this window: a prefix of its npiv launched ones
+  for (int s = 0; s < npiv; ++s) madeK += win.made[s];
+  double p[K];
+#pragma unroll
+  for (int s = 0; s < K; ++s) p[s] = win.rec[(int64_t)(live ? kr : 0) * RECW + 2 + s];
+  // (loaded before the made-count check: a slot not made in this window holds a
+  // stale value, so the index is clamped; such values are never used)
+  for (int x = threadIdx.x; x < K * K; x += BLK) {
+    const int L = x / K, s = x % K;
+    const int64_t rl = min(max(win.r[L] - row0, (int64_t)0), m_local - 1);
+    fr[L][s] = win.F[(int64_t)s * ld + rl];
+  }
+  if (threadIdx.x < K) {
+    const int64_t r = win.r[threadIdx.x];
+    bool last = true;  // the last leaving slot of row r among the made ones
+    for (int s = threadIdx.x + 1; s < madeK; ++s) last &= win.r[s] != r;
+    rows[threadIdx.x] = r - row0;
+    lastL[threadIdx.x] = last;
+  }
+  __syncthreads();
+  if (madeK == 0 || !live || !fast) return;
+#pragma unroll
+  for (int L = 0; L < K; ++L) {
+    if (L >= madeK || !lastL[L] || rows[L] < 0 || rows[L] >= m_local) continue;  // not ours
+    double x = p[L];
+#pragma unroll
+    for (int s = L + 1; s < K; ++s)
+      if (s < madeK) x = msub(x, fr[L][s], p[s]);
+    __builtin_nontemporal_store(x, A + j * ld + rows[L]);  // scattered 8-B writes: no L2 allocate
+  }
 }
 
 }  // namespace spx

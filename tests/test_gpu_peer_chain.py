@@ -1,4 +1,4 @@
-"""The row-sharded persistent chain (chain_kernel<.., SH = true>).
+"""The row-sharded persistent chain (chain_shard_kernel).
 
 Each rank runs ONE persistent launch per window over its row block; the ratio
 records of every rank's blocks are written to every rank's record buffer, and
@@ -75,19 +75,21 @@ def _check_vs_oracle(outs, kind, m, n, seed, rule, max_iters=200000):
     (1, "dense", 200, 300, "dantzig", 8),
     (2, "dense", 200, 300, "dantzig", 8),
     (3, "dense", 301, 257, "dantzig", 24),
-    (4, "dense", 1024, 2048, "dantzig", 16),
+    (3, "dense", 1024, 2048, "dantzig", 16),
     (2, "degenerate", 64, 64, "bland", 12),
     (3, "degenerate", 96, 96, "bland", 32),
-    (4, "dense", 7, 9, "dantzig", 4),   # ranks with one or two rows
-    (5, "dense", 7, 9, "dantzig", 4),   # > 4 virtual ranks: launch-per-phase (see below)
+    (3, "dense", 7, 9, "dantzig", 4),   # ranks with two or three rows
+    (4, "dense", 7, 9, "dantzig", 4),   # >= 4 virtual ranks: launch-per-phase (see below)
+    (5, "dense", 7, 9, "dantzig", 4),
 ])
 def test_peer_chain_virtual_ranks_bit_exact(world, kind, m, n, rule, K):
     """Virtual ranks are streams of one process, which get GPU_MAX_HW_QUEUES
     (4) hardware queues: two chains on one queue would run one after the
-    other and wait for each other's records, so more than 4 virtual ranks on a
-    GPU take the launch-per-phase path (chain_blocks 0), same bytes."""
+    other and wait for each other's records, so with one queue kept for the
+    process's other streams, 4 or more virtual ranks on a GPU take the
+    launch-per-phase path (chain_blocks 0), same bytes."""
     outs = _peer_threads(world, kind, m, n, 3, rule, K)
-    if world <= 4:
+    if world <= 3:
         assert all(o[6] >= 1 for o in outs.values()), "the persistent sharded chain did not run"
     else:
         assert all(o[6] == 0 for o in outs.values())

@@ -5,7 +5,7 @@ own basis entries and the shared objective row.
 
   single        the single-GPU engine on one 1024-row block (N = 1 kernels)
   rccl1         1-rank RCCL communicator: prep -> all-gather -> finish per pivot
-  peer1         1-rank row-sharded persistent chain (chain_kernel<.., SH>)
+  peer1         1-rank row-sharded persistent chain (chain_shard_kernel)
   peer2v/peer3v 2 / 3 virtual ranks (threads, one stream each) of 1024 rows,
                 the row-sharded persistent chain: ratio records to every rank,
                 row gather from the owner's tableau (in-process peers)
