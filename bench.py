@@ -79,7 +79,7 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=15.0,
                     help="budget of the CPU-baseline sample (0 disables)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles",
-                                                           "traffic_r02.json"))
+                                                           "traffic_r03.json"))
     return ap.parse_args()
 
 
