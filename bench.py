@@ -323,10 +323,12 @@ def main():
                  "window": f"HIP events around the chain of {c_n} windows run after the "
                            f"timed region"}
     what = "flush (window pass)" if K else "elimination"
+    between = every - 1
     every = f"every {every}th"
     window = (f"timed region: HIP events on the engine stream around {every} {what}, "
-              f"launched directly" + ("; the other windows replay the per-window hipGraph"
-                                      if (use_graph and K) else ""))
+              f"launched directly" + (f"; the windows in between replay one hipGraph of "
+                                      f"{between} windows" if (use_graph and K and between)
+                                      else ""))
     avg_ms = ms_tot / launches
     m_local = row1 - row0
     N = n + m + 1
@@ -381,8 +383,8 @@ def main():
                                     else f"config 4: config-3 tableau row-sharded x{world}"),
                        "m": m, "n": n, "tableau": [m + 1, N], "rule": args.rule,
                        "elimination": "dense sweep" if args.dense else "skip p[j]==0 columns",
-                       "timing": ("per-window hipGraph replay" if (use_graph and K)
-                                  else "direct launches"),
+                       "timing": ("hipGraph replay (several windows per graph)"
+                                  if (use_graph and K) else "direct launches"),
                        "elim_variant": fvar,
                        "step": (f"one tableau pass = a window of {K} pivots" if K
                                 else "one pivot (single-pivot elimination pass)"),

@@ -155,8 +155,14 @@ struct spx_ctx {
   int peer_same_dev = 1;        // ranks whose chains share this rank's GPU
 
   // graph cache
-  hipGraphExec_t gexec = nullptr;
-  int gchunk = 0;
+  // captured launch sequences by chunk (pivots): a few sizes per context
+  // (the bench's warmup and timed runs, spx_solve), so none is rebuilt inside
+  // a timed region
+  std::map<int, hipGraphExec_t> graphs;
+  hipGraphExec_t gexec = nullptr;  // the one build_graph returned last
+  // windows per replayed graph (SPX_GRAPH_WINDOWS): consecutive windows in one
+  // graph pay one graph-launch gap (8.4 us at config 3) instead of one each
+  int graph_windows = 4;
 
   // elimination timing
   std::vector<std::pair<hipEvent_t, hipEvent_t>> ev;
@@ -204,9 +210,9 @@ void dfree(T*& p) {
 }
 
 void drop_graphs(spx_ctx* ctx) {
-  if (ctx->gexec) (void)hipGraphExecDestroy(ctx->gexec);
+  for (auto& kv : ctx->graphs) (void)hipGraphExecDestroy(kv.second);
+  ctx->graphs.clear();
   ctx->gexec = nullptr;
-  ctx->gchunk = 0;
 }
 
 void close_peers(spx_ctx* ctx) {
@@ -697,8 +703,16 @@ int enqueue_pivot(spx_ctx* ctx, bool time_elim) {
 // or npiv fused single-pivot steps.  `time_k` > 0 brackets eliminations (or
 // flushes) with events: every time_k-th elimination / window.
 int enqueue_pivots(spx_ctx* ctx, int npiv, int time_k, int64_t first = 0) {
-  if (ctx->win_k)
-    return enqueue_window(ctx, npiv, time_k > 0 && (first / ctx->win_k) % time_k == 0);
+  if (ctx->win_k) {  // consecutive windows of win_k pivots (the last may be shorter)
+    for (int done = 0; done < npiv;) {
+      const int n = std::min(ctx->win_k, npiv - done);
+      const int rc =
+          enqueue_window(ctx, n, time_k > 0 && ((first + done) / ctx->win_k) % time_k == 0);
+      if (rc) return rc;
+      done += n;
+    }
+    return SPX_OK;
+  }
   for (int i = 0; i < npiv; ++i) {
     const int rc = enqueue_pivot(ctx, time_k > 0 && (first + i) % time_k == 0);
     if (rc) return rc;
@@ -766,8 +780,11 @@ int begin_call(spx_ctx* ctx, const spx_opts* o, AdmCall* adm_call, int64_t fc = 
 }
 
 int build_graph(spx_ctx* ctx, int chunk) {
-  if (ctx->gexec && ctx->gchunk == chunk) return SPX_OK;
-  if (ctx->gexec) (void)hipGraphExecDestroy(ctx->gexec);
+  const auto it = ctx->graphs.find(chunk);
+  if (it != ctx->graphs.end()) {
+    ctx->gexec = it->second;
+    return SPX_OK;
+  }
   ctx->gexec = nullptr;
   hipGraph_t g = nullptr;
   HIPC(hipStreamBeginCapture(ctx->stream, hipStreamCaptureModeThreadLocal));
@@ -788,7 +805,7 @@ int build_graph(spx_ctx* ctx, int chunk) {
     ctx->err = std::string("hipGraphInstantiate: ") + hipGetErrorString(e);
     return SPX_E_HIP;
   }
-  ctx->gchunk = chunk;
+  ctx->graphs[chunk] = ctx->gexec;
   return SPX_OK;
 }
 
@@ -933,6 +950,9 @@ int spx_create(spx_ctx** out, int device) {
   // tuning hook: SPX_FLUSH_TAIL=x (0..50) overrides the flush's tail share
   if (const char* ft = std::getenv("SPX_FLUSH_TAIL"))
     ctx->flush_tail = std::max(0, std::min(50, std::atoi(ft)));
+  // windows per replayed graph (1..16; tuning hook)
+  if (const char* gw = std::getenv("SPX_GRAPH_WINDOWS"))
+    ctx->graph_windows = std::max(1, std::min(16, std::atoi(gw)));
   *out = ctx;
   return SPX_OK;
 }
@@ -1332,7 +1352,8 @@ int spx_solve(spx_ctx* ctx, const spx_opts* opts, spx_result* res) {
   int rc = begin_call(ctx, o, &adm_call);
   if (rc) return rc;
   const int64_t it0 = ctx->h_st->iters;
-  const int chunk = ctx->win_k ? ctx->win_k : (o->chunk > 0 ? o->chunk : 32);
+  const int chunk =
+      ctx->win_k ? ctx->win_k * ctx->graph_windows : (o->chunk > 0 ? o->chunk : 32);
   const bool use_graph = o->use_graph != 0 && !ctx->loop && !ctx->time_chain;
   if (use_graph) {
     rc = build_graph(ctx, chunk);
@@ -1461,22 +1482,30 @@ int spx_run_pivots(spx_ctx* ctx, const spx_opts* opts, int64_t npivots, int time
     // (One graph of the whole request ran 18 % slower at config 3: a hipGraph
     // of ~550 nodes is submitted in batches the GPU overtakes.)
     if (!ctx->win_k || !graph) return enqueue_all(time_elim);
-    if ((rc = build_graph(ctx, ctx->win_k))) return rc;
+    // the untimed windows between two timed ones replay one graph of
+    // time_elim - 1 windows (a shorter run: launched directly)
+    const int run = std::max(1, std::min(time_elim - 1, ctx->graph_windows));
+    if ((rc = build_graph(ctx, run * ctx->win_k))) return rc;
     int64_t done = 0;
-    for (int64_t w = 0; done < npivots; ++w) {
+    for (int64_t w = 0; done < npivots;) {
       const int n = (int)std::min<int64_t>(ctx->win_k, npivots - done);
       const bool timed = w % time_elim == 0;
-      if (n == ctx->win_k && !timed) {
+      if (!timed && time_elim > 1 && npivots - done >= (int64_t)run * ctx->win_k &&
+          (w % time_elim) + run <= time_elim) {
         HIPC(hipGraphLaunch(ctx->gexec, ctx->stream));
-      } else if ((rc = enqueue_window(ctx, n, timed))) {
-        return rc;
+        done += (int64_t)run * ctx->win_k;
+        w += run;
+        continue;
       }
+      if ((rc = enqueue_window(ctx, n, timed))) return rc;
       done += n;
+      ++w;
     }
     return SPX_OK;
   }
   if (!time_elim && graph) {
-    const int chunk = ctx->win_k ? ctx->win_k : (o->chunk > 0 ? o->chunk : 32);
+    const int chunk =
+        ctx->win_k ? ctx->win_k * ctx->graph_windows : (o->chunk > 0 ? o->chunk : 32);
     if ((rc = build_graph(ctx, chunk))) return rc;
     int64_t left = npivots;
     for (; left >= chunk; left -= chunk) HIPC(hipGraphLaunch(ctx->gexec, ctx->stream));

@@ -8,7 +8,15 @@ config 3 / 4).  One JSON line per config:
   config 5: degenerate 4096 x 4096 LP, Bland's rule: pivots/s over K pivots on
             one GPU vs the C/OpenMP oracle over its first pivots (same
             sequence checked).
-Both GPU results are checked against the oracle (objective / pivot sequence).
+  full solves (--full): config 3's Dantzig solve to optimality (22,169
+            pivots) and config 5's 100,000-pivot Bland prefix on one GPU at
+            K = 24, wall time of spx_solve with the tableau resident, beside
+            the pinned fixture's oracle and HiGHS 'highs-ds' wall times
+            (tests/golden/fullsize.json: measured in the dev container, 4
+            oracle threads; HiGHS takes minutes there, so it is not re-run
+            on the GPU box).  The GPU's pivot count and objective must equal
+            the fixture's bit for bit.
+All GPU results are checked against the oracle (objective / pivot sequence).
 """
 import json
 import os
@@ -79,6 +87,37 @@ def config5(window=0, k=2048, k_cpu=60):
             "first_pivots_match_oracle": [tuple(x) for x in hist[:len(hc)]] == hc}
 
 
+def full_solve(name, window=24):
+    fx = json.load(open(os.path.join(ROOT, "tests", "golden", "fullsize.json")))[name]
+    cap = fx.get("max_pivots", 0)
+    Tf, obj, basis = synth.tableau_rows(fx["kind"], fx["m"], fx["n"], fx["seed"], order="F")
+    with DeviceTableau(0) as e:
+        e.set_window(window)
+        e.load_rows(Tf, obj, basis, fx["m"], 0)
+        e.solve(rule=fx["rule"], max_iters=2 * window)  # warm: graphs, first launches
+        e.load_rows(Tf, obj, basis, fx["m"], 0)
+        del Tf
+        t0 = time.perf_counter()
+        res = e.solve(rule=fx["rule"], max_iters=cap)
+        gpu_s = time.perf_counter() - t0
+    return {"config": f"{name}: {fx['m']}x{fx['n']} {fx['kind']} LP, {fx['rule']}, "
+                      + (f"first {cap} pivots" if cap else "solve to optimality"),
+            "window": window, "gpu_s": gpu_s, "pivots": res.iters,
+            "gpu_pivots_per_s": res.iters / gpu_s, "status": res.status,
+            "objective": res.objective, "matches_fixture": res.iters == fx["pivots"]
+            and res.objective == fx["objective"],
+            "oracle_s_dev_container": fx.get("oracle_seconds"),
+            "oracle_threads_dev_container": fx.get("oracle_threads"),
+            "highs_s_dev_container": fx.get("highs_seconds"), "highs_nit": fx.get("highs_nit"),
+            "highs_objective": fx.get("highs_objective"),
+            "highs_note": "HiGHS solves the LP to optimality (a different algorithm)"
+                          + ("; the GPU runs the fixture's Bland prefix" if cap else "")}
+
+
 if __name__ == "__main__":
+    if "--full" in sys.argv:
+        for name in ("config3", "config5"):
+            print(json.dumps(full_solve(name)), flush=True)
+        sys.exit(0)
     for fn, w in ((config2, 0), (config2, 8), (config2, 24), (config5, 0), (config5, 16), (config5, 24)):
         print(json.dumps(fn(w)), flush=True)
