@@ -207,7 +207,7 @@ int spx_get_elim_variant(const spx_ctx* ctx, int64_t out[7]);
  * of the last flush launch (0 before the first flush). */
 int spx_get_flush_variant(const spx_ctx* ctx, int64_t out[4]);
 /* Windowed ("delayed") elimination: apply K pivots per streaming pass over
- * the tableau (K in 2, 4, 8, 12, 16, 24, 32; 0 or 1 = one pass per pivot).
+ * the tableau (K in 2, 4, 8, 12, 16, 24, 28, 32; 0 or 1 = one pass per pivot).
  * Results are bit-identical.  Row-sharded contexts run the
  * same windows with one all-gather per pivot. */
 int spx_set_window(spx_ctx* ctx, int K);

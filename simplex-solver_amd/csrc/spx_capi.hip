@@ -664,6 +664,7 @@ int enqueue_window(spx_ctx* ctx, int npiv, bool time_flush) {
     case 12: return enqueue_window_t<12>(ctx, npiv, time_flush);
     case 16: return enqueue_window_t<16>(ctx, npiv, time_flush);
     case 24: return enqueue_window_t<24>(ctx, npiv, time_flush);
+    case 28: return enqueue_window_t<28>(ctx, npiv, time_flush);
     default: return enqueue_window_t<32>(ctx, npiv, time_flush);
   }
 }
@@ -1547,9 +1548,9 @@ int spx_probe_flush_grid(spx_ctx* ctx, int* rch, int* G) {
 
 int spx_set_window(spx_ctx* ctx, int K) {
   if (!ctx) return SPX_E_ARG;
-  CHECK_ARG(K == 0 || K == 1 || K == 2 || K == 4 || K == 8 || K == 12 || K == 16 || K == 24 ||
+  CHECK_ARG(K == 0 || K == 1 || K == 2 || K == 4 || K == 8 || K == 12 || K == 16 || K == 24 || K == 28 ||
                 K == 32,
-            "window must be 0, 1, 2, 4, 8, 12, 16, 24 or 32");
+            "window must be 0, 1, 2, 4, 8, 12, 16, 24, 28 or 32");
   ctx->win_k = K <= 1 ? 0 : K;
   drop_graphs(ctx);
   return SPX_OK;

@@ -44,7 +44,7 @@ def _run(eng_cls, T, basis, K, mode, min_blocks=0, **kw):
         return res, e.history().tolist(), e.tableau(), e.basis(), blocks
 
 
-@pytest.mark.parametrize("K", [2, 8, 16, 24, 32])
+@pytest.mark.parametrize("K", [2, 8, 16, 24, 28, 32])
 @pytest.mark.parametrize("shape", [(2, 3), (17, 40), (300, 700), (1025, 2051)])
 @pytest.mark.parametrize("rule", ["dantzig", "bland"])
 @pytest.mark.parametrize("mode", [2, 3], ids=["cb256", "cb512"])

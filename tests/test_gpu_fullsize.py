@@ -72,10 +72,12 @@ def _full_solve(name, window=24):
     return fx
 
 
-def test_config3_dantzig_full_solve_pinned():
+@pytest.mark.parametrize("window", [24, 28])
+def test_config3_dantzig_full_solve_pinned(window):
     """Config 3 (8192 x 8192 dense LP, tableau 8193 x 16385): the whole
-    Dantzig solve at K = 24 vs the oracle's, index for index."""
-    _full_solve("config3")
+    Dantzig solve at K = 24 and at the bench's K = 28 vs the oracle's, index
+    for index."""
+    _full_solve("config3", window=window)
 
 
 def test_config5_bland_100k_pivots_pinned():
@@ -118,7 +120,7 @@ def test_config5_bland_million_pivots_no_basis_repeats():
     assert zobrist_repeats(h, basis) == 0
 
 
-@pytest.mark.parametrize("window", [24])
+@pytest.mark.parametrize("window", [24, 28])
 def test_config4_eight_virtual_ranks_240_pivots_pinned(window):
     """Config 4: the config-3 tableau row-sharded over 8 ranks (1024 rows
     each; virtual ranks on one GPU), 10 windows of 24 pivots: the pivot

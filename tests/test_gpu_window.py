@@ -42,7 +42,7 @@ def _run(eng_cls, T, basis, K, **kw):
         return res, e.history().tolist(), e.tableau(), e.basis()
 
 
-@pytest.mark.parametrize("K", [2, 8, 12, 16, 24, 32])
+@pytest.mark.parametrize("K", [2, 8, 12, 16, 24, 28, 32])
 @pytest.mark.parametrize("shape", [(2, 3), (17, 40), (300, 700), (1025, 2051)])
 @pytest.mark.parametrize("skip", [True, False], ids=["skip", "dense"])
 def test_window_rule_pivots_bit_exact(eng_cls, K, shape, skip):
@@ -65,7 +65,7 @@ def _set_flush_map(e, fmap):
 
 
 @pytest.mark.parametrize("fmap", [0, 1, 2, 3])
-@pytest.mark.parametrize("K", [2, 12, 16, 24, 32])
+@pytest.mark.parametrize("K", [2, 12, 16, 24, 28, 32])
 @pytest.mark.parametrize("shape", [(17, 40), (700, 1500), (1537, 2600)])
 def test_window_flush_block_maps_bit_exact(eng_cls, fmap, K, shape):
     """The LDS-DMA flush under every block map (group-major, chunk-major,
@@ -249,10 +249,10 @@ def test_window_ld_padding_and_odd_rows(eng_cls, pad):
 
 def test_window_sizes_validated(eng_cls):
     with eng_cls(0) as e:
-        for bad in (3, 5, 10, 20, 33, 64, -1):
+        for bad in (3, 5, 10, 20, 30, 33, 64, -1):
             with pytest.raises(Exception):
                 e.set_window(bad)
-        for good in (0, 1, 2, 4, 8, 12, 16, 24, 32):
+        for good in (0, 1, 2, 4, 8, 12, 16, 24, 28, 32):
             e.set_window(good)
 
 
