@@ -74,8 +74,9 @@ def parse():
                          "all-gather per pivot")
     ap.add_argument("--time-every", type=int, default=0,
                     help="HIP events around every k-th elimination (or window flush) of the "
-                         "timed region (0: 8 eliminations / 4 flushes; an event node costs "
-                         "~6 us of stream time)")
+                         "timed region (0: every 8th elimination / flush; an event node costs "
+                         "~6 us of stream time, and a timed window is launched directly: "
+                         "~21 us per timed window at config 3)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0,
                     help="budget of the CPU-baseline sample (0 disables)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles",
@@ -288,7 +289,7 @@ def main():
     barrier()
     eng.sync()
     t0 = time.perf_counter()
-    every = args.time_every if args.time_every > 0 else (4 if K else 8)
+    every = args.time_every if args.time_every > 0 else 8
     eng.run_pivots(n_timed, time_elim=every, **opts)
     eng.sync()
     t1 = time.perf_counter()
