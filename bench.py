@@ -327,9 +327,9 @@ def main():
     between = every - 1
     every = f"every {every}th"
     window = (f"timed region: HIP events on the engine stream around {every} {what}, "
-              f"launched directly" + (f"; the windows in between replay one hipGraph of "
-                                      f"{between} windows" if (use_graph and K and between)
-                                      else ""))
+              f"launched directly" + ("; of the windows in between, runs of 4 replay one "
+                                      "hipGraph (SPX_GRAPH_WINDOWS), the rest are launched "
+                                      "directly" if (use_graph and K and between) else ""))
     avg_ms = ms_tot / launches
     m_local = row1 - row0
     N = n + m + 1
