@@ -1478,20 +1478,21 @@ int spx_run_pivots(spx_ctx* ctx, const spx_opts* opts, int64_t npivots, int time
     return SPX_OK;
   };
   if (time_elim) {
-    // Timed: untimed windows replay the per-window graph; every time_elim-th
-    // window (or elimination) is launched directly between two stream events.
+    // Timed: every time_elim-th window (or elimination) is launched directly
+    // between two stream events; the untimed windows replay graphs (below).
     // (One graph of the whole request ran 18 % slower at config 3: a hipGraph
     // of ~550 nodes is submitted in batches the GPU overtakes.)
     if (!ctx->win_k || !graph) return enqueue_all(time_elim);
-    // the untimed windows between two timed ones replay one graph of
-    // time_elim - 1 windows (a shorter run: launched directly)
-    const int run = std::max(1, std::min(time_elim - 1, ctx->graph_windows));
-    if ((rc = build_graph(ctx, run * ctx->win_k))) return rc;
+    // the untimed windows between two timed ones replay the graph of
+    // graph_windows windows (the one an untimed call builds, so no graph is
+    // captured inside a timed region); shorter runs are launched directly
+    const int run = ctx->graph_windows;
+    if (time_elim > run && (rc = build_graph(ctx, run * ctx->win_k))) return rc;
     int64_t done = 0;
     for (int64_t w = 0; done < npivots;) {
       const int n = (int)std::min<int64_t>(ctx->win_k, npivots - done);
       const bool timed = w % time_elim == 0;
-      if (!timed && time_elim > 1 && npivots - done >= (int64_t)run * ctx->win_k &&
+      if (!timed && time_elim > run && npivots - done >= (int64_t)run * ctx->win_k &&
           (w % time_elim) + run <= time_elim) {
         HIPC(hipGraphLaunch(ctx->gexec, ctx->stream));
         done += (int64_t)run * ctx->win_k;
