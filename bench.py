@@ -21,6 +21,7 @@ workload, 1 thread, rank 0 at N=1 only).
 from __future__ import annotations
 
 import argparse
+import hashlib
 import json
 import os
 import sys
@@ -72,6 +73,10 @@ def parse():
                     help="N > 1 windows: 1 the row-sharded persistent chain (peer records over "
                          "xGMI, after a bit-exact self-test against the RCCL path), 0 one RCCL "
                          "all-gather per pivot")
+    ap.add_argument("--same-device", action="store_true",
+                    help="N > 1 rehearsal on ONE GPU: every rank on GPU 0, peer-only shards "
+                         "(no RCCL, IPC-mapped peers), the self-test against the single-GPU "
+                         "path; exercises the whole N > 1 bench path before an 8-GPU node")
     ap.add_argument("--time-every", type=int, default=0,
                     help="HIP events around every k-th elimination (or window flush) of the "
                          "timed region (0: every 8th elimination / flush; an event node costs "
@@ -184,13 +189,15 @@ def _host_cpus():
             "affinity_cpus": aff, "OMP_NUM_THREADS": os.environ.get("OMP_NUM_THREADS")}
 
 
-def peer_selftest(eng, world, rank, K, tdist, torch):
+def peer_selftest(eng, world, rank, K, tdist, torch, same_device=False):
     """Before the timed run: the row-sharded persistent chain must reproduce the
     RCCL launch-per-phase path byte for byte on a small LP (every rank, all
-    ranks agree), else the bench falls back to RCCL.  Returns (ok, note)."""
+    ranks agree), else the bench falls back to RCCL.  --same-device (peer-only
+    shards, no RCCL): the reference is the single-GPU windowed path on the
+    whole LP, and a failure ends the bench.  Returns (ok, note)."""
     from simplex_amd import synth
     from simplex_amd.dist import row_partition
-    from simplex_amd.engine import SpxError
+    from simplex_amd.engine import DeviceTableau, SpxError
 
     def all_ok(flag):
         t = torch.tensor([1 if flag else 0], dtype=torch.int64)
@@ -214,6 +221,19 @@ def peer_selftest(eng, world, rank, K, tdist, torch):
         ok, note = False, f"peer chain failed: {ex}"
     if not all_ok(ok):  # (every rank leaves here together: no collective is left pending)
         return False, note if not ok else "peer chain failed on another rank"
+    if same_device:
+        Tw, objw, bw = synth.tableau_rows("dense", ms, ns, 99, 0, ms, order="F")
+        with DeviceTableau(0) as ref:
+            ref.set_window(K)
+            ref.load_rows(Tw, objw, bw, ms, 0)
+            ref.solve(**kw)
+            full = ref.tableau()
+            hist = ref.history()
+        mine = np.vstack([full[r0:r1], full[-1:]])
+        same = (hist.tobytes(), mine.tobytes()) == a
+        ok = all_ok(same)
+        return ok, ("ok (vs the single-GPU path)" if ok else
+                    "peer chain differs from the single-GPU path")
     eng.set_chain(1)  # the RCCL all-gather path on the same LP
     eng.load_rows(T, obj, basis, ms, r0)
     eng.solve(**kw)
@@ -239,7 +259,14 @@ def main():
     if not torch.cuda.is_available():
         raise SystemExit("bench.py needs a GPU (HIP); none visible")
     m, n = args.m, args.n
-    if world > 1:
+    if args.same_device and world < 2:
+        raise SystemExit("--same-device needs WORLD_SIZE >= 2 (torch.distributed.run)")
+    if world > 1 and args.same_device:
+        # rehearsal of the N > 1 path on one GPU: no RCCL (it refuses two ranks
+        # on one device), the peers IPC-mapped
+        tdist.init_process_group("gloo")
+        eng = ShardedTableau(0, rank, world, None, local="peer")
+    elif world > 1:
         tdist.init_process_group("gloo")
         uid = exchange_unique_id()
         eng = ShardedTableau(local, rank, world, uid)
@@ -254,9 +281,13 @@ def main():
     if K:
         eng.set_window(K)
     peer = None
+    if args.same_device and not (K and args.peer):
+        raise SystemExit("--same-device runs the peer chain only (--window > 1, --peer 1)")
     if world > 1 and K and args.peer:
-        ok, note = peer_selftest(eng, world, rank, K, tdist, torch)
+        ok, note = peer_selftest(eng, world, rank, K, tdist, torch, args.same_device)
         peer = {"enabled": ok, "selftest": note}
+        if args.same_device and not ok:
+            raise SystemExit(f"--same-device: {note}")
     if world == 1:
         eng.set_chain(args.chain, args.chain_blocks)
     elif peer is None or not peer["enabled"]:
@@ -356,9 +387,9 @@ def main():
     except (OSError, ValueError):
         pass
 
-    hist = eng.history() if (rank == 0 and world == 1 and args.cpu_seconds > 0) else None
+    hist = eng.history() if rank == 0 else None
     cpu = None
-    if hist is not None:
+    if hist is not None and world == 1 and args.cpu_seconds > 0:
         cpu = cpu_baseline(m, n, args.seed, args.rule, args.cpu_seconds, hist.tolist())
     if rank == 0:
         value = n_timed / elapsed
@@ -381,7 +412,9 @@ def main():
             "data": f"synthetic: hash-seeded dense random-feasible LP (simplex_amd.synth, "
                     f"seed {args.seed})",
             "config": {"workload": ("config 3: 8192x16384 fp64 dense tableau" if world == 1
-                                    else f"config 4: config-3 tableau row-sharded x{world}"),
+                                    else f"config 4: config-3 tableau row-sharded x{world}"
+                                    + (" (rehearsal: every rank on GPU 0)" if args.same_device
+                                       else "")),
                        "m": m, "n": n, "tableau": [m + 1, N], "rule": args.rule,
                        "elimination": "dense sweep" if args.dense else "skip p[j]==0 columns",
                        "timing": ("hipGraph replay (several windows per graph)"
@@ -391,6 +424,7 @@ def main():
                                 else "one pivot (single-pivot elimination pass)"),
                        "window": K,
                        "chain_blocks": eng.chain_blocks(),
+                       "same_device": bool(args.same_device),
                        "parallelism": ("single GPU" if world == 1 else
                                        f"row-shard x{world}, " + (
                                            "one persistent chain launch per window, ratio "
@@ -410,6 +444,11 @@ def main():
             "chain": chain,
             "cpu_baseline": cpu,
             "objective_after": z,
+            # every pivot of the run (warmup, timed, chain timing) from the
+            # slack basis: tests compare it with the oracle's fixture
+            "pivots_total": int(len(hist)),
+            "pivots_sha256": hashlib.sha256(
+                np.ascontiguousarray(hist, dtype="<i8").tobytes()).hexdigest(),
         }
         print(json.dumps(line), flush=True)
     eng.close()

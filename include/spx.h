@@ -227,17 +227,34 @@ int spx_set_chain(spx_ctx* ctx, int mode, int min_blocks);
 /* Blocks of the persistent chain the loaded tableau uses (0: not used). */
 int spx_get_chain(spx_ctx* ctx, int* blocks);
 /* Admission of persistent chains: a persistent chain needs all
- * of its blocks resident at once, so the process admits, per device, chains
+ * of its blocks resident at once, so the processes on a device admit chains
  * whose blocks in flight fit a budget (default: the device's CU count, or the
  * SPX_CHAIN_BUDGET environment variable); a call that does not fit runs its
  * windows with the launch-per-phase chain, bit-identical.  This makes the
  * reference's concurrent /solve calls (tests/test_performance_load.py:80,190,268)
  * slow down instead of failing.  blocks < 0 restores the default; 0 forces the
- * launch-per-phase chain (e.g. several processes sharing one GPU). */
+ * launch-per-phase chain. */
 int spx_set_chain_budget(int device, int blocks);
+/* The budget is shared by every process using the same GPU through a table in
+ * /dev/shm (entries {pid, blocks} under flock; dead processes' entries free;
+ * SPX_CHAIN_SHM=0 turns it off).  This writes the table's path for `device`
+ * (at most cap bytes with the terminating NUL). */
+int spx_chain_shm_path(int device, char* out, int cap);
 /* A context's admission record: out[0] calls run with the persistent chain,
  * out[1] calls refused (launch-per-phase chain), out[2] blocks held now. */
 int spx_get_chain_stats(spx_ctx* ctx, int64_t out[3]);
+/* Start handshake of persistent chains ("Residency"): before
+ * its first store every block of a chain announces itself and waits at most
+ * `us` microseconds for all the others (0 = automatic: 20 us on one GPU, 100 ms
+ * for row shards, whose ranks enqueue independently).  If some block is not
+ * resident (its CU held by another kernel or process, or another chain ahead
+ * of it on the same hardware queue), no block stores anything, the window
+ * reports ST_NOTRES, and spx_solve / spx_pivot / spx_pivot_at rerun it with
+ * the launch-per-phase chain (peer-only shards: the persistent chain again),
+ * bit-identical.  us < 0 makes every persistent window abort (test hook). */
+int spx_set_chain_handshake(spx_ctx* ctx, int64_t us);
+/* Windows the context reran after such an abort. */
+int spx_get_chain_reruns(spx_ctx* ctx, int64_t* n);
 /* Layout knob: extra doubles of padding per stored column (even, 0..4096);
   * applies to the next spx_load / spx_load_rows; -1 = automatic. */
 int spx_set_ld_pad(spx_ctx* ctx, int pad);

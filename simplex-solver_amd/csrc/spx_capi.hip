@@ -17,8 +17,15 @@
 // broadcast, without a host-known root).
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
+#include <errno.h>
+#include <fcntl.h>
+#include <signal.h>
+#include <sys/file.h>
+#include <sys/stat.h>
+#include <unistd.h>
 
 #include <algorithm>
+#include <cctype>
 #include <chrono>
 #include <condition_variable>
 #include <cstdio>
@@ -153,6 +160,13 @@ struct spx_ctx {
   std::vector<void*> ipc_open;  // IPC-mapped peer buffers (closed on reload / destroy)
   ChainPeers* d_peers = nullptr;  // device copy of `peers` (the chain kernel's argument)
   int peer_same_dev = 1;        // ranks whose chains share this rank's GPU
+  int peer_B = 0, peer_cb = BLK;  // the shard chain's grid, agreed by every rank at import
+
+  // start handshake of persistent chains (spx_chain.hpp chain_start): bound in
+  // us (0: automatic, < 0: force ABORT, a test hook), and the windows rerun
+  // after a chain found its blocks not co-resident (ST_NOTRES)
+  int64_t hs_us = 0;
+  int64_t chain_reruns = 0;
 
   // graph cache
   // captured launch sequences by chunk (pivots): a few sizes per context
@@ -221,6 +235,7 @@ void close_peers(spx_ctx* ctx) {
   ctx->peer_ok = false;
   ctx->peers = ChainPeers{};
   ctx->peer_same_dev = 1;
+  ctx->peer_B = 0;
 }
 
 int free_buffers(spx_ctx* ctx) {
@@ -415,51 +430,54 @@ int lazy_ratio_grid(const spx_ctx* ctx) {
   return std::max(1, (int)((ctx->m_local + BLK - 1) / BLK));
 }
 
-// Hardware queues of this process (HIP's GPU_MAX_HW_QUEUES, default 4).
-int hw_queues() {
-  const char* e = std::getenv("GPU_MAX_HW_QUEUES");
-  const int v = e ? std::atoi(e) : 0;
-  return v > 0 ? v : 4;
-}
-
 // Persistent chain geometry: B blocks of CB threads (one per CU, all
 // resident), each owning <= CB columns and <= CB rows.  Returns B (and CB in
 // *cb), or 0 when the chain does not apply (row shards, the launch-per-phase
 // mode, or a tableau wider than CB x CUs columns).  mode 2 / 3 force 256- /
 // 512-thread blocks; automatic: 256 threads (measured faster than 512 at
 // config 3, profiles/r02), 512 when the tableau needs more than 256 blocks.
+int device_cus(int device) {
+  int n = 0;
+  if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess ||
+      n <= 0)
+    n = 256;
+  return n;
+}
+
+// Threads per chain block for a grid of `wide` columns / rows: 256 (measured
+// faster than 512 at config 3, profiles/r02) unless the tableau needs more
+// than 256 blocks of them; chain modes 2 / 3 force 256 / 512.
+int chain_cb(int mode, int64_t wide, int n_cu) {
+  return mode == 2 ? 256 : mode == 3 ? 512
+         : (wide > 256 * std::min(n_cu, CHAIN_MAX_BLOCKS) ? 512 : 256);
+}
+
+// Blocks of a chain of cb threads over N columns and `rows` rows: the N-1
+// candidate columns set the width (the RHS column rides along with the last
+// block's last thread when B * cpb == N - 1, spx_chain.hpp xown).
+int64_t chain_need(int64_t N, int64_t rows, int cb, int min_blocks) {
+  return std::max<int64_t>({(N - 1 + cb - 1) / cb, (rows + cb - 1) / cb, 1, (int64_t)min_blocks});
+}
+
+// Persistent chain geometry: B blocks of CB threads (one per CU, all
+// resident), each owning <= CB columns and <= CB rows.  Returns B (and CB in
+// *cb), or 0 when the chain does not apply (the launch-per-phase mode, a
+// refused admission, or a tableau wider than CB x CUs columns).  Row shards
+// take the geometry every rank agreed on at spx_peer_import /
+// spx_peer_chain_local (shard_geometry), so no rank decides alone.
 int chain_blocks(spx_ctx* ctx, int* cb_out = nullptr, bool ignore_admission = false) {
   if (ctx->chain_mode == 1) return 0;
-  if (ctx->sharded && !ctx->peer_ok) return 0;  // shards: only once the peers are known
+  if (ctx->sharded) {  // shards: only once the peers are known
+    if (!ctx->peer_ok) return 0;
+    if (cb_out) *cb_out = ctx->peer_cb;
+    return ctx->chain_denied ? 0 : ctx->peer_B;
+  }
   if (ctx->chain_denied && !ignore_admission) return 0;
-  if (!ctx->n_cu) {
-    (void)hipDeviceGetAttribute(&ctx->n_cu, hipDeviceAttributeMultiprocessorCount, ctx->device);
-    if (ctx->n_cu <= 0) ctx->n_cu = 256;
-  }
-  // row shards: one grid geometry on every rank (B from the largest row
-  // block), so every rank decides the same way
-  const int64_t rows =
-      ctx->sharded ? (ctx->m_global + ctx->nranks - 1) / ctx->nranks : ctx->m_local;
-  const int64_t wide = std::max<int64_t>(ctx->N, rows);
-  const int cb = ctx->chain_mode == 2 ? 256 : ctx->chain_mode == 3 ? 512
-                 : (wide > 256 * std::min(ctx->n_cu, CHAIN_MAX_BLOCKS) ? 512 : 256);
+  if (!ctx->n_cu) ctx->n_cu = device_cus(ctx->device);
+  const int cb = chain_cb(ctx->chain_mode, std::max<int64_t>(ctx->N, ctx->m_local), ctx->n_cu);
   if (cb_out) *cb_out = cb;
-  // the N-1 candidate columns set the width: the RHS column rides along with
-  // the last block's last thread when B * cpb == N - 1 (spx_chain.hpp, xown)
-  const int64_t need = std::max<int64_t>({(ctx->N - 1 + cb - 1) / cb, (rows + cb - 1) / cb,
-                                          1, (int64_t)ctx->chain_min_blocks});
+  const int64_t need = chain_need(ctx->N, ctx->m_local, cb, ctx->chain_min_blocks);
   const int64_t cap = std::min<int64_t>((int64_t)ctx->n_cu, CHAIN_MAX_BLOCKS);
-  if (ctx->sharded) {  // every rank's records in one poll; the chains sharing a GPU all resident
-    // virtual ranks: one process's streams share its hardware queues
-    // (GPU_MAX_HW_QUEUES, 4 by default), and two chains on one queue run one
-    // after the other -- each would wait for the other's records forever.  One
-    // queue stays for the process's other streams (the default stream once
-    // used, other contexts): with 4 virtual ranks beside it, two ranks' chains
-    // shared a queue and timed out (round 3)
-    if (ctx->loop && ctx->peer_same_dev >= hw_queues()) return 0;
-    return need * ctx->nranks <= CHAIN_SH_SLOTS && need * ctx->peer_same_dev <= cap ? (int)need
-                                                                                      : 0;
-  }
   return need <= cap ? (int)need : 0;
 }
 
@@ -471,16 +489,113 @@ int chain_blocks(spx_ctx* ctx, int* cb_out = nullptr, bool ignore_admission = fa
 // CU count; SPX_CHAIN_BUDGET or spx_set_chain_budget override it) runs its
 // windows with the launch-per-phase chain instead, which is bit-identical and
 // needs no co-residency.  So concurrent /solve calls slow down instead of
-// timing out.  Other processes on the same GPU are not seen: give each its
-// share with SPX_CHAIN_BUDGET (0 forces the launch-per-phase chain).
+// timing out.
+//
+// Across processes (gunicorn's two workers, /root/reference/dockerfile:34)
+// the budget is shared through a table in /dev/shm/spx_chain_<PCI bus id>: 64
+// entries {pid, blocks}, read and written under flock.  Each process keeps
+// its entry equal to its in-flight blocks on that GPU; a chain is admitted
+// only when every live process's blocks plus its own fit the budget.  Entries
+// of dead processes (kill(pid, 0) -> ESRCH) count as free, and a process
+// clears its entries at exit.  SPX_CHAIN_SHM=0 turns the table off (the
+// process-local count still applies); the start handshake (chain_start) is
+// the backstop for GPU users outside this scheme.
+constexpr int SHM_SLOTS = 64;
+struct ShmEntry {
+  int32_t pid, blocks;
+};
+
+struct ShmTable {
+  int fd = -1;
+  pid_t opener = 0;  // fds inherited across fork() share their flock: reopen
+  std::string path;
+};
+
+std::string shm_path(int device) {
+  char bus[64] = {0};
+  if (hipDeviceGetPCIBusId(bus, (int)sizeof(bus) - 1, device) != hipSuccess)
+    std::snprintf(bus, sizeof(bus), "dev%d", device);
+  std::string p = "/dev/shm/spx_chain_";
+  for (const char* c = bus; *c; ++c) p += std::isalnum((unsigned char)*c) ? *c : '_';
+  return p;
+}
+
 struct ChainAdmission {
   std::mutex mu;
   std::map<int, int> used;    // chain blocks in flight, by device
   std::map<int, int> budget;  // explicit budgets (spx_set_chain_budget)
+  std::map<int, ShmTable> shm;
+  ~ChainAdmission();
 };
 ChainAdmission& adm() {
   static ChainAdmission a;
   return a;
+}
+
+bool shm_enabled() {
+  const char* e = std::getenv("SPX_CHAIN_SHM");
+  return !(e && e[0] == '0');
+}
+
+// The device's table, opened by this process (-1: unavailable).
+int shm_fd_locked(ChainAdmission& a, int device) {
+  ShmTable& t = a.shm[device];
+  if (t.fd >= 0 && t.opener == getpid()) return t.fd;
+  if (t.fd >= 0) close(t.fd);  // inherited across fork(): its flock is the parent's
+  t.fd = -1;
+  if (!shm_enabled()) return -1;
+  if (t.path.empty()) t.path = shm_path(device);
+  t.fd = open(t.path.c_str(), O_RDWR | O_CREAT | O_CLOEXEC, 0666);
+  // every process (user) on the GPU shares the table: 0666 regardless of the
+  // umask (fchmod, not a process-wide umask change; fails harmlessly when
+  // another user created the file)
+  if (t.fd >= 0) (void)fchmod(t.fd, 0666);
+  t.opener = getpid();
+  return t.fd;
+}
+
+// Under the table's flock: the blocks of every OTHER live process, and (when
+// mine >= 0) this process's entry set to `mine`.  Returns -1 when the table
+// is unavailable (the process-local count then decides alone).
+int shm_exchange(int fd, int mine) {
+  if (fd < 0) return -1;
+  if (flock(fd, LOCK_EX) != 0) return -1;
+  ShmEntry e[SHM_SLOTS];
+  std::memset(e, 0, sizeof(e));
+  const ssize_t got = pread(fd, e, sizeof(e), 0);
+  (void)got;  // (a short or new file reads as free entries)
+  const int32_t me = (int32_t)getpid();
+  int others = 0, slot = -1, free_slot = -1;
+  bool dirty = false;
+  for (int x = 0; x < SHM_SLOTS; ++x) {
+    if (e[x].pid == me) {
+      slot = x;
+    } else if (e[x].pid > 0 && e[x].blocks > 0) {
+      if (kill(e[x].pid, 0) == 0 || errno == EPERM) {
+        others += e[x].blocks;
+      } else {  // a dead process's entry: free it
+        e[x] = ShmEntry{0, 0};
+        dirty = true;
+      }
+    }
+    if (free_slot < 0 && (e[x].pid <= 0 || e[x].blocks <= 0) && e[x].pid != me) free_slot = x;
+  }
+  if (mine >= 0) {
+    if (slot < 0) slot = free_slot;
+    if (slot >= 0) {
+      e[slot] = ShmEntry{mine > 0 ? me : 0, mine};
+      dirty = true;
+    }
+  }
+  if (dirty) (void)!pwrite(fd, e, sizeof(e), 0);
+  flock(fd, LOCK_UN);
+  return others;
+}
+
+ChainAdmission::~ChainAdmission() {
+  // normal exit: this process's entries go back to the tables
+  for (auto& kv : shm)
+    if (kv.second.fd >= 0 && kv.second.opener == getpid()) (void)shm_exchange(kv.second.fd, 0);
 }
 
 int adm_budget_locked(ChainAdmission& a, const spx_ctx* ctx) {
@@ -495,9 +610,6 @@ int adm_budget_locked(ChainAdmission& a, const spx_ctx* ctx) {
 bool adm_acquire(spx_ctx* ctx) {
   const bool was = ctx->chain_denied;
   ctx->chain_denied = false;
-  // row shards own their GPUs and must all take the same chain: not admitted
-  // per process
-  if (ctx->sharded) return false;
   const int B = ctx->win_k ? chain_blocks(ctx, nullptr, true) : 0;
   if (B <= 0) return false;  // no persistent chain for this call anyway
   ChainAdmission& a = adm();
@@ -507,7 +619,16 @@ bool adm_acquire(spx_ctx* ctx) {
     const int cap = adm_budget_locked(a, ctx);
     int& used = a.used[ctx->device];
     const int extra = std::max(0, B - ctx->adm_blocks);  // 0: this context holds B already
-    ok = used + extra <= cap;
+    // row shards must all take the same chain: never refused,
+    // but their blocks count against the device's budget while they run, so
+    // single-GPU chains beside them are refused instead of over-subscribing
+    ok = ctx->sharded || used + extra <= cap;
+    if (ok && extra > 0) {  // the other processes' chains on this GPU (the shared table)
+      const int fd = shm_fd_locked(a, ctx->device);
+      const int others = shm_exchange(fd, -1);
+      ok = ctx->sharded || others < 0 || others + used + extra <= cap;
+      if (ok && fd >= 0) (void)shm_exchange(fd, used + extra);
+    }
     if (ok) {
       used += extra;
       ctx->adm_blocks += extra;
@@ -524,7 +645,9 @@ void adm_release(spx_ctx* ctx) {
   ChainAdmission& a = adm();
   std::lock_guard<std::mutex> lk(a.mu);
   if (ctx->adm_calls > 0 && --ctx->adm_calls == 0) {
-    a.used[ctx->device] -= ctx->adm_blocks;
+    int& used = a.used[ctx->device];
+    used -= ctx->adm_blocks;
+    if (ctx->adm_blocks > 0) (void)shm_exchange(shm_fd_locked(a, ctx->device), used);
     ctx->adm_blocks = 0;
   }
 }
@@ -737,11 +860,23 @@ int write_params(spx_ctx* ctx, const spx_opts* o) {
   return SPX_OK;
 }
 
+// Start-handshake bound of persistent chains, in s_memrealtime ticks (100 MHz):
+// 20 us on one GPU (the grid's blocks are dispatched together), 100 ms for row
+// shards (the ranks' hosts enqueue their windows independently, so a rank's
+// chain may start that much after another's); spx_set_chain_handshake
+// overrides it (< 0: every persistent window aborts, a test hook).
+int64_t hs_ticks(const spx_ctx* ctx) {
+  if (ctx->hs_us < 0) return -1;
+  if (ctx->hs_us > 0) return ctx->hs_us * 100;
+  return ctx->sharded ? 10000000 : 2000;
+}
+
 // Host-side writes of State fields (synchronous; between pivot calls only).
 int set_state_fields(spx_ctx* ctx, int32_t status, int64_t fc, int64_t fr) {
   ctx->h_st->status = status;
   ctx->h_st->forced_c = fc;
   ctx->h_st->forced_r = fr;
+  ctx->h_st->hs_ticks = hs_ticks(ctx);
   HIPC(hipMemcpyAsync(ctx->st, ctx->h_st, sizeof(State), hipMemcpyHostToDevice, ctx->stream));
   return SPX_OK;
 }
@@ -815,17 +950,54 @@ int map_status(int32_t st) {
     case ST_OPTIMAL: return SPX_OPTIMAL;
     case ST_UNBOUNDED: return SPX_UNBOUNDED;
     case ST_LIMIT: return SPX_ITER_LIMIT;
-    case ST_FAULT: return SPX_E_STATE;
+    case ST_FAULT:
+    case ST_NOTRES: return SPX_E_STATE;
     default: return SPX_RUNNING;
   }
 }
 
-bool is_fault(int32_t st) { return st == ST_FAULT; }
+bool is_fault(int32_t st) { return st == ST_FAULT || st == ST_NOTRES; }
 
-// The device reported a fault (an in-launch exchange timed out).
+// The device reported a fault (an in-launch exchange timed out), or a window
+// that did not run (ST_NOTRES) where the call could not rerun it.
 int fault(spx_ctx* ctx) {
-  ctx->err = "device fault: a pivot-chain exchange timed out (blocks not co-resident?)";
+  if (ctx->h_st->status == ST_NOTRES)
+    ctx->err = "a persistent chain's blocks were not co-resident, so its window did not run "
+               "(spx_run_pivots does not rerun it; spx_solve / spx_pivot do)";
+  else
+    ctx->err = "device fault: a pivot-chain exchange timed out";
   return SPX_E_STATE;
+}
+
+// Reruns of a window whose persistent chain aborted at its start handshake
+// before a peer-only shard (no launch-per-phase path) gives up.
+constexpr int NOTRES_RETRIES = 16;
+
+// A persistent chain found its blocks not co-resident (ST_NOTRES, spx_chain.hpp
+// chain_start): nothing of that window ran, and every later launch of the call
+// exited at once.  Resume the call where it stopped (the stream is drained):
+// the next window epoch (the aborted one's handshake words keep their
+// verdict), status RUNNING with the call's forced pivot, and the rest of the
+// call on the launch-per-phase chain, which needs no co-residency -- or, for a
+// peer-only shard, which has no such path, the persistent chain again.
+int notres_resume(spx_ctx* ctx, int64_t fc, int64_t fr, int* retries) {
+  ctx->chain_reruns++;
+  const bool lazy_ok = !ctx->sharded || ctx->comm || ctx->loop;
+  if (!lazy_ok && ++*retries > NOTRES_RETRIES) {
+    ctx->err = "persistent chain: blocks not co-resident after repeated reruns (peer-only "
+               "shard: no launch-per-phase path)";
+    return SPX_E_STATE;
+  }
+  uint32_t e = 0;
+  HIPC(hipMemcpyAsync(&e, ctx->win.epoch, sizeof(e), hipMemcpyDeviceToHost, ctx->stream));
+  HIPC(hipStreamSynchronize(ctx->stream));
+  e = (e + 1u) & TAG_EPOCH;
+  HIPC(hipMemcpyAsync(ctx->win.epoch, &e, sizeof(e), hipMemcpyHostToDevice, ctx->stream));
+  if (lazy_ok && !ctx->chain_denied) {
+    ctx->chain_denied = true;
+    drop_graphs(ctx);
+  }
+  return set_state_fields(ctx, ST_RUNNING, fc, fr);
 }
 
 int alloc_common(spx_ctx* ctx, int64_t m_local, int64_t N, int64_t m_global, int64_t row0) {
@@ -871,9 +1043,10 @@ int alloc_common(spx_ctx* ctx, int64_t m_local, int64_t N, int64_t m_global, int
     // shards: every rank's records, two parity halves and the window-end plane
     // (peers write them over xGMI: uncached, so this GPU's L2 never serves a
     // stale copy to the local polls; plain memory between virtual ranks)
+    // (+2 planes: the start handshake's arrivals and verdict word)
     const size_t gq = sizeof(unsigned long long) *
-                      (ctx->sharded ? (size_t)CHAIN_SH_PLANES * CHAIN_SH_SLOTS
-                                    : (size_t)RATIO_REC * CHAIN_MAX_BLOCKS);
+                      (ctx->sharded ? (size_t)(HS_PLANE_SHARD + 2) * CHAIN_SH_SLOTS
+                                    : (size_t)(HS_PLANE_1GPU + 2) * CHAIN_MAX_BLOCKS);
     HIPC(hipMalloc(&ctx->gr_enter, ge));
     if (ctx->sharded && !ctx->loop) {
       if (hipExtMallocWithFlags((void**)&ctx->gr_ratio, gq, hipDeviceMallocUncached) != hipSuccess) {
@@ -1035,18 +1208,77 @@ struct PeerBlob {
   hipIpcMemHandle_t hA, hR;  // this rank's tableau and ratio-record buffer
   int64_t ld, row0, m_local, N, m_global;
   char bus[64];              // PCI bus id: which ranks share a GPU
+  int32_t n_cu, chain_mode, chain_min_blocks, pad;  // what the shard geometry depends on
 };
-constexpr uint32_t PEER_MAGIC = 0x53505850u;  // "SPXP"
+constexpr uint32_t PEER_MAGIC = 0x53505851u;  // "SPXQ" (round 4 layout)
+
+// What one rank contributes to the shard chain's geometry (its blob, or a
+// virtual rank's context): every rank computes the geometry from ALL ranks'
+// inputs, in rank order, so every rank reaches the same decision.
+struct ShardIn {
+  std::string dev;  // device key (PCI bus id): the ranks sharing a GPU form a group
+  int n_cu = 0, mode = 0, min_blocks = 0;
+  int64_t m_local = 0;
+};
+
+// Device groups (ranks sharing a GPU: one start handshake each, their chains
+// resident together) and the grid of the row-sharded chain.  B = 0 when the
+// grid does not fit: every rank's records in one poll (nranks * B <= 512) and
+// each group's blocks on its GPU's CUs.  Rows per block come from the LARGEST
+// row block (an uneven split may give a rank more rows than the even share:
+// every row must be owned by one thread of its block).
+int shard_geometry(spx_ctx* ctx, ChainPeers& pe, const std::vector<ShardIn>& in, int* B_out,
+                   int* cb_out) {
+  const int nr = pe.nranks;
+  for (int q = 1; q < nr; ++q)
+    CHECK_ARG(in[q].mode == in[0].mode && in[q].min_blocks == in[0].min_blocks,
+              "peer chain: ranks disagree on the chain mode (spx_set_chain)");
+  pe.ngroups = 0;
+  int gof[CHAIN_MAX_RANKS];
+  for (int q = 0; q < nr; ++q) {
+    int g = -1;
+    for (int h = 0; h < pe.ngroups && g < 0; ++h)
+      if (in[pe.gleader[h]].dev == in[q].dev) g = h;
+    if (g < 0) {
+      g = pe.ngroups++;
+      pe.gleader[g] = q;
+      pe.gmask[g] = 0u;
+    }
+    pe.gmask[g] |= 1u << q;
+    gof[q] = g;
+  }
+  pe.group = gof[pe.rank];
+  int64_t rows = 0;
+  int cu_min = CHAIN_MAX_BLOCKS;
+  for (const ShardIn& x : in) {
+    rows = std::max(rows, x.m_local);
+    cu_min = std::min(cu_min, x.n_cu > 0 ? x.n_cu : 256);
+  }
+  const int cb = chain_cb(in[0].mode, std::max<int64_t>(ctx->N, rows), cu_min);
+  const int64_t need = chain_need(ctx->N, rows, cb, in[0].min_blocks);
+  bool ok = in[0].mode != 1 && need * nr <= CHAIN_SH_SLOTS;
+  for (int g = 0; g < pe.ngroups; ++g) {
+    int cap = CHAIN_MAX_BLOCKS;
+    for (int q = 0; q < nr; ++q)
+      if ((pe.gmask[g] >> q) & 1u) cap = std::min(cap, in[q].n_cu > 0 ? in[q].n_cu : 256);
+    ok = ok && need * __builtin_popcount(pe.gmask[g]) <= cap;
+  }
+  *B_out = ok ? (int)need : 0;
+  *cb_out = cb;
+  return SPX_OK;
+}
 
 // Install a peers table: host copy, device copy (with this rank's stop word), on.
-int peer_commit(spx_ctx* ctx, const ChainPeers& pe, int same_dev) {
+int peer_commit(spx_ctx* ctx, const ChainPeers& pe, int B, int cb) {
   ctx->peers = pe;
   ctx->peers.stop_req = (const int32_t*)ctx->d_stop;
   if (!ctx->d_peers) HIPC(hipMalloc(&ctx->d_peers, sizeof(ChainPeers)));
   HIPC(hipMemcpyAsync(ctx->d_peers, &ctx->peers, sizeof(ChainPeers), hipMemcpyHostToDevice,
                       ctx->stream));
   HIPC(hipStreamSynchronize(ctx->stream));
-  ctx->peer_same_dev = same_dev;
+  ctx->peer_same_dev = __builtin_popcount(pe.gmask[pe.group]);
+  ctx->peer_B = B;
+  ctx->peer_cb = cb;
   ctx->peer_ok = true;
   drop_graphs(ctx);
   return SPX_OK;
@@ -1084,6 +1316,10 @@ int spx_peer_export(spx_ctx* ctx, void* out, int64_t cap) {
   b.N = ctx->N;
   b.m_global = ctx->m_global;
   HIPC(hipDeviceGetPCIBusId(b.bus, (int)sizeof(b.bus) - 1, ctx->device));
+  if (!ctx->n_cu) ctx->n_cu = device_cus(ctx->device);
+  b.n_cu = ctx->n_cu;
+  b.chain_mode = ctx->chain_mode;
+  b.chain_min_blocks = ctx->chain_min_blocks;
   std::memcpy(out, &b, sizeof(b));
   return SPX_OK;
 }
@@ -1100,17 +1336,29 @@ int spx_peer_import(spx_ctx* ctx, const void* blobs, int nranks) {
   close_peers(ctx);
   HIPC(hipSetDevice(ctx->device));
   const PeerBlob* bl = static_cast<const PeerBlob*>(blobs);
-  const PeerBlob& me = bl[ctx->rank];
   ChainPeers pe{};
   pe.rank = ctx->rank;
   pe.nranks = nranks;
-  int same = 0;
+  std::vector<ShardIn> in(nranks);
+  int64_t rows_sum = 0;
   for (int q = 0; q < nranks; ++q) {
     const PeerBlob& b = bl[q];
     CHECK_ARG(b.magic == PEER_MAGIC && b.rank == q && b.nranks == nranks && b.N == ctx->N &&
-                  b.m_global == ctx->m_global,
-              "peer import: blob mismatch (rank order, shape)");
-    same += std::strncmp(b.bus, me.bus, sizeof(b.bus)) == 0 ? 1 : 0;
+                  b.m_global == ctx->m_global && b.m_local >= 0,
+              "peer import: blob mismatch (rank order, shape, library version)");
+    CHECK_ARG(b.row0 == rows_sum, "peer import: the ranks' row blocks must tile 0..m in rank order");
+    rows_sum += b.m_local;
+    in[q].dev = std::string(b.bus, strnlen(b.bus, sizeof(b.bus)));
+    in[q].n_cu = b.n_cu;
+    in[q].mode = b.chain_mode;
+    in[q].min_blocks = b.chain_min_blocks;
+    in[q].m_local = b.m_local;
+  }
+  CHECK_ARG(rows_sum == ctx->m_global, "peer import: the row blocks do not cover every row");
+  int B = 0, cb = BLK;
+  if ((rc = shard_geometry(ctx, pe, in, &B, &cb))) return rc;
+  for (int q = 0; q < nranks; ++q) {
+    const PeerBlob& b = bl[q];
     pe.ld[q] = b.ld;
     pe.row0[q] = b.row0;
     if (q == ctx->rank) {
@@ -1132,7 +1380,7 @@ int spx_peer_import(spx_ctx* ctx, const void* blobs, int nranks) {
     pe.A[q] = static_cast<const double*>(pa);
     pe.ratio[q] = static_cast<unsigned long long*>(pr);
   }
-  return peer_commit(ctx, pe, same);
+  return peer_commit(ctx, pe, B, cb);
 }
 
 // Virtual ranks (spx_create_sharded_local): the peers are this process's
@@ -1147,20 +1395,37 @@ int spx_peer_chain_local(spx_ctx* ctx) {
   ChainPeers pe{};
   pe.rank = ctx->rank;
   pe.nranks = ctx->nranks;
-  int same = 0;
+  std::vector<ShardIn> in(G->n);
+  int64_t rows_sum = 0;
+  // (every rank checks the same members in the same order, so all return the
+  // same error before the second barrier, or none does)
   for (int q = 0; q < G->n; ++q) {
     spx_ctx* m = G->members[q];
     CHECK_ARG(m && m->loaded && m->N == ctx->N && m->m_global == ctx->m_global,
               "spx_peer_chain_local: group member not loaded / shape mismatch");
+    // the chain dereferences the members' tableaux and record buffers as
+    // plain device pointers: no peer mapping between GPUs here
+    CHECK_ARG(m->device == G->members[0]->device,
+              "spx_peer_chain_local: virtual ranks of a peer chain must share one GPU "
+              "(use one process per GPU and spx_peer_export / spx_peer_import)");
+    CHECK_ARG(m->row0 == rows_sum, "spx_peer_chain_local: row blocks must tile 0..m in rank order");
+    rows_sum += m->m_local;
     pe.A[q] = m->A;
     pe.ratio[q] = m->gr_ratio;
     pe.ld[q] = m->ld;
     pe.row0[q] = m->row0;
-    same += m->device == ctx->device ? 1 : 0;
+    in[q].dev = std::to_string(m->device);
+    in[q].n_cu = device_cus(m->device);
+    in[q].mode = m->chain_mode;
+    in[q].min_blocks = m->chain_min_blocks;
+    in[q].m_local = m->m_local;
   }
+  CHECK_ARG(rows_sum == ctx->m_global, "spx_peer_chain_local: row blocks do not cover every row");
+  int B = 0, cb = BLK;
+  if ((rc = shard_geometry(ctx, pe, in, &B, &cb))) return rc;
   if (!G->barrier()) return loop_fail(ctx);  // nobody reloads while the others read
   close_peers(ctx);
-  return peer_commit(ctx, pe, same);
+  return peer_commit(ctx, pe, B, cb);
 }
 
 int spx_destroy(spx_ctx* ctx) {
@@ -1377,10 +1642,19 @@ int spx_solve(spx_ctx* ctx, const spx_opts* opts, spx_result* res) {
     HIPC(hipEventRecord(ctx->ev_poll[i & 1], ctx->stream));
     return SPX_OK;
   };
+  int retries = 0;
   if ((rc = launch_chunk(0))) return rc;
   for (int64_t i = 0;; ++i) {
     if ((rc = launch_chunk(i + 1))) return rc;
     HIPC(hipEventSynchronize(ctx->ev_poll[i & 1]));
+    if (ctx->h_poll[i & 1].status == ST_NOTRES) {
+      // a window's chain was not co-resident: drain (chunk i+1 only exits
+      // early), resume, and restart the pipeline with chunk i+1
+      if ((rc = pull_state(ctx)) || (rc = notres_resume(ctx, -1, -1, &retries))) return rc;
+      if (use_graph && (rc = build_graph(ctx, chunk))) return rc;
+      if ((rc = launch_chunk(i + 1))) return rc;
+      continue;
+    }
     status = map_status(ctx->h_poll[i & 1].status);
     if (status != SPX_RUNNING) break;
     const double el =
@@ -1420,8 +1694,12 @@ int spx_pivot(spx_ctx* ctx, const spx_opts* opts, int64_t* r, int64_t* c) {
   int rc = begin_call(ctx, opts, &adm_call);
   if (rc) return rc;
   const int64_t it0 = ctx->h_st->iters;
-  if ((rc = enqueue_pivots(ctx, 1, 0))) return rc;
-  if ((rc = pull_state(ctx))) return rc;
+  for (int retries = 0;;) {
+    if ((rc = enqueue_pivots(ctx, 1, 0))) return rc;
+    if ((rc = pull_state(ctx))) return rc;
+    if (ctx->h_st->status != ST_NOTRES) break;
+    if ((rc = notres_resume(ctx, -1, -1, &retries))) return rc;
+  }
   adm_call.drained = true;
   const int status = map_status(ctx->h_st->status);
   if (status < 0) return fault(ctx);
@@ -1442,9 +1720,13 @@ int spx_pivot_at(spx_ctx* ctx, int64_t r, int64_t c) {
   AdmCall adm_call(ctx);
   int rc = begin_call(ctx, nullptr, &adm_call, c, r);
   if (rc) return rc;
-  if ((rc = enqueue_pivots(ctx, 1, 0))) return rc;
-  // pull the post-pivot state before writing the forced fields back
-  if ((rc = pull_state(ctx))) return rc;
+  // (pull the post-pivot state before writing the forced fields back)
+  for (int retries = 0;;) {
+    if ((rc = enqueue_pivots(ctx, 1, 0))) return rc;
+    if ((rc = pull_state(ctx))) return rc;
+    if (ctx->h_st->status != ST_NOTRES) break;
+    if ((rc = notres_resume(ctx, c, r, &retries))) return rc;
+  }
   adm_call.drained = true;
   const int32_t st_after = ctx->h_st->status;
   if (is_fault(st_after)) return fault(ctx);
@@ -1753,6 +2035,33 @@ int spx_get_flush_variant(const spx_ctx* ctx, int64_t out[4]) {
   out[1] = ctx->flush_map;
   out[2] = ctx->last_flush_rch;
   out[3] = ctx->last_flush_G;
+  return SPX_OK;
+}
+
+// Path of the cross-process admission table of `device` (DESIGN.md §4b,
+// "Admission"), e.g. for an operator to inspect or clear it.
+int spx_chain_shm_path(int device, char* out, int cap) {
+  if (!out || cap <= 0) return SPX_E_ARG;
+  const std::string p = shm_path(device);
+  if ((int)p.size() >= cap) return SPX_E_ARG;
+  std::memcpy(out, p.c_str(), p.size() + 1);
+  return SPX_OK;
+}
+
+// Start handshake of persistent chains (spx_chain.hpp chain_start): bound in
+// us (0 = automatic: 20 us on one GPU, 100 ms for row shards); < 0 makes every
+// persistent window abort at its start, so the call reruns it (test hook).
+int spx_set_chain_handshake(spx_ctx* ctx, int64_t us) {
+  if (!ctx) return SPX_E_ARG;
+  ctx->hs_us = us;
+  return SPX_OK;
+}
+
+// Windows this context reran after their persistent chain found its blocks
+// not co-resident (ST_NOTRES).
+int spx_get_chain_reruns(spx_ctx* ctx, int64_t* n) {
+  if (!ctx || !n) return SPX_E_ARG;
+  *n = ctx->chain_reruns;
   return SPX_OK;
 }
 

@@ -61,6 +61,7 @@ __device__ unsigned long long spx_probe_chain[32 * 4 * 256];
 #endif
 
 constexpr int32_t ST_FAULT = 5;       // a chain exchange timed out (never on a healthy GPU)
+constexpr int32_t ST_NOTRES = 6;      // a chain's blocks were not all resident: its window did not run
 // Records are stored granule-major: granule g of block b at rec[g * CHAIN_MAX_BLOCKS + b],
 // so one poll instruction of a wave reads 64 blocks' granule g as 512 contiguous bytes.
 // A record is a polled header plus extras that only the winner's record is read for
@@ -79,6 +80,12 @@ constexpr unsigned CHAIN_SPIN_MAX = 1u << 22;
 constexpr int CHAIN_MAX_RANKS = 16;
 constexpr int CHAIN_SH_SLOTS = 512;     // nranks x B ratio records (8 per polling lane)
 constexpr int CHAIN_SH_PLANES = 2 * RATIO_REC + 1;
+// Start handshake planes (chain_start): one arrival granule per block, then
+// the verdict word (slot 0 of the next plane).  Single GPU: after the ratio
+// records of gr_ratio; row shards: after CHAIN_SH_PLANES, in the buffer of the
+// rank that leads the caller's device group.
+constexpr int HS_PLANE_1GPU = RATIO_REC;
+constexpr int HS_PLANE_SHARD = CHAIN_SH_PLANES;
 
 typedef __attribute__((address_space(1))) unsigned long long gu64;
 typedef __attribute__((address_space(1))) unsigned gu32;
@@ -101,11 +108,17 @@ __device__ __forceinline__ unsigned long long g_load(const gu64* g) {
 // processes, plain device pointers between the virtual ranks of one process).
 struct ChainPeers {
   int rank, nranks;
-  unsigned long long* ratio[CHAIN_MAX_RANKS];  // CHAIN_SH_PLANES x CHAIN_SH_SLOTS granules each
+  unsigned long long* ratio[CHAIN_MAX_RANKS];  // (CHAIN_SH_PLANES + 2) x CHAIN_SH_SLOTS granules each
   const double* A[CHAIN_MAX_RANKS];
   int64_t ld[CHAIN_MAX_RANKS];
   int64_t row0[CHAIN_MAX_RANKS];
   const int32_t* stop_req;  // rank 0: the host's time-limit stop request (pinned)
+  // device groups (ranks sharing a GPU) for the start handshake: group g's
+  // lowest rank gleader[g] holds its arrival plane and verdict word; gmask[g]
+  // has a bit per member rank; `group` is this rank's
+  int ngroups, group;
+  int gleader[CHAIN_MAX_RANKS];
+  uint32_t gmask[CHAIN_MAX_RANKS];
 };
 // write-through (sc1) store / load of one double
 __device__ __forceinline__ void wt_store(double* p, double v) {
@@ -241,6 +254,81 @@ __device__ __forceinline__ bool spin_fail(unsigned& spins, State* st) {
     __hip_atomic_store((gu32*)&st->status, (unsigned)ST_FAULT, __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_AGENT);
   return true;
+}
+
+constexpr int GK_START = 3;  // a block's arrival at the start handshake (chain_start)
+
+// Start handshake of a persistent chain launch ("Residency").
+// The chain's exchanges need every block of the launch resident at once; a
+// block that is not (its CU held by another kernel, another chain queued in
+// front of it on the same hardware queue) would leave the others spinning.
+// Before its first store every block stores an arrival granule (tag: window
+// epoch W, kind GK_START), and wave 0 polls its device group's arrivals for
+// at most `bound` ticks of s_memrealtime (100 MHz).  The outcome is fixed ONCE
+// per group and window by a compare-and-swap on the group's verdict word,
+// from the value of an earlier window to (W, GO) -- every arrival seen -- or
+// (W, ABORT) -- the wait ran out: the first CAS wins and every block, late
+// ones included, reads the same verdict.  So either every block runs the
+// window or none stores anything; on ABORT the host reruns the window
+// (ST_NOTRES).  A verdict word already past W means W was aborted (no group
+// runs a later window before every group finished W).  Row shards with several
+// device groups also wait for every group's verdict: the window runs only
+// when all said GO.  Returns 0 go, 1 abort, 2 fault (a group never decided
+// within ~4 s).  Wave 0 only: the caller hands the result to its block.
+template <bool SYS>
+__device__ __forceinline__ int chain_start(const gu64* arr, int nslots, int B, uint32_t gmask,
+                                           gu64* vword, uint32_t W, int64_t bound,
+                                           uint64_t t0, const ChainPeers* pe, State* st) {
+  const int lane = threadIdx.x & 63;
+  const unsigned tag = rec_tag(W, 0, GK_START);
+  bool late = bound < 0;  // (a negative bound forces ABORT: the rerun test hook)
+  for (unsigned spins = 0; !late;) {
+    bool ok = true;
+    for (int x = lane; x < nslots; x += 64)
+      if ((gmask >> (x / B)) & 1u) ok &= (unsigned)(g_load<SYS>(arr + x) >> 32) == tag;
+    if (__all(ok)) break;
+    late = (int64_t)(__builtin_amdgcn_s_memrealtime() - t0) > bound;
+    if (!late && spin_fail(spins, st)) return 2;
+  }
+  unsigned v = 0u;
+  if (lane == 0) {
+    const unsigned long long want = ((unsigned long long)W << 8) | (late ? 2u : 1u);
+    unsigned long long cur = g_load<SYS>(vword);
+    for (;;) {
+      const int32_t d = (int32_t)((uint32_t)(cur >> 8) - W);
+      if (d > 0) {  // the group is past W: W was aborted
+        cur = 2u;
+        break;
+      }
+      if (d == 0) break;  // decided by another block
+      if (__hip_atomic_compare_exchange_strong(vword, &cur, want, __ATOMIC_RELAXED,
+                                               __ATOMIC_RELAXED,
+                                               SYS ? __HIP_MEMORY_SCOPE_SYSTEM
+                                                   : __HIP_MEMORY_SCOPE_AGENT)) {
+        cur = want;
+        break;
+      }
+    }
+    v = (unsigned)(cur & 0xffu);
+  }
+  v = __shfl(v, 0, 64);
+  if (v != 1u) return 1;
+  if (pe == nullptr || pe->ngroups <= 1) return 0;
+  // every other device group's verdict (system-scope loads of their words)
+  for (unsigned spins = 0;;) {
+    bool dec = true, ab = false;
+    if (lane < pe->ngroups) {
+      const gu64* w = (const gu64*)pe->ratio[pe->gleader[lane]] +
+                      (size_t)(HS_PLANE_SHARD + 1) * CHAIN_SH_SLOTS;
+      const unsigned long long x = g_load<true>(w);
+      const int32_t d = (int32_t)((uint32_t)(x >> 8) - W);
+      dec = d >= 0;
+      ab = d > 0 || (d == 0 && (x & 0xffu) == 2u);
+    }
+    if (__any(ab)) return 1;
+    if (__all(dec)) return 0;
+    if (spin_fail(spins, st)) return 2;
+  }
 }
 
 // Poll the B record headers of one phase (lane l reads blocks l, l+64, ...)
@@ -522,6 +610,7 @@ __global__ __launch_bounds__(CB) void chain_kernel(
   const int64_t forced_r = st->forced_r;
   const int64_t it0 = st->iters;
   const int64_t hist_cap = st->hist_cap;
+  const int64_t hs_bound = st->hs_ticks;
   const uint32_t E = *win.epoch;
   const int32_t rule = prm->rule;
   const double eps_piv = prm->eps_piv;
@@ -569,6 +658,26 @@ __global__ __launch_bounds__(CB) void chain_kernel(
     if (leader)
       for (int s = 0; s < npiv; ++s) win.made[s] = 0;  // (the flush counts made slots)
     return;
+  }
+  {
+    // start handshake: every block resident, or nothing of this window runs
+    gu64* hs = gr_ratio + (size_t)HS_PLANE_1GPU * CHAIN_MAX_BLOCKS;
+    const uint64_t t_hs = __builtin_amdgcn_s_memrealtime();
+    __shared__ int hs_res;
+    if (t == 0) g_store(hs + b, rec_tag(W, 0, GK_START), 0u);
+    if (w0) {
+      const int res = chain_start<false>(hs, B, B, 1u, hs + CHAIN_MAX_BLOCKS, W, hs_bound, t_hs,
+                                         nullptr, st);
+      if (t == 0) hs_res = res;
+    }
+    __syncthreads();
+    if (hs_res != 0) {  // (2: ST_FAULT is stored already)
+      if (leader) {
+        if (hs_res == 1) st->status = ST_NOTRES;
+        for (int s = 0; s < npiv; ++s) win.made[s] = 0;
+      }
+      return;
+    }
   }
   if (leader) {
     // the flush's record counter; reset write-through and drained before this
@@ -1034,6 +1143,7 @@ __global__ __launch_bounds__(CB) void chain_shard_kernel(
   const int64_t forced_r = st->forced_r;
   const int64_t it0 = st->iters;
   const int64_t hist_cap = st->hist_cap;
+  const int64_t hs_bound = st->hs_ticks;
   const uint32_t E = *win.epoch;
   const int32_t rule = prm->rule;
   const double eps_piv = prm->eps_piv;
@@ -1104,6 +1214,29 @@ __global__ __launch_bounds__(CB) void chain_shard_kernel(
     if (leader)
       for (int s = 0; s < npiv; ++s) win.made[s] = 0;  // (the flush counts made slots)
     return;
+  }
+  {
+    // start handshake over this rank's device group (the ranks sharing its
+    // GPU), then every group's verdict: every block of every rank resident, or
+    // nothing of this window runs on any rank
+    const int grp = pe->group;
+    gu64* hs = (gu64*)pe->ratio[pe->gleader[grp]] + (size_t)HS_PLANE_SHARD * RS;
+    const uint64_t t_hs = __builtin_amdgcn_s_memrealtime();
+    __shared__ int hs_res;
+    if (t == 0) g_store<true>(hs + bs, rec_tag(W, 0, GK_START), 0u);
+    if (w0) {
+      const int res = chain_start<true>(hs, BR, B, pe->gmask[grp], hs + RS, W, hs_bound, t_hs,
+                                        pe, st);
+      if (t == 0) hs_res = res;
+    }
+    __syncthreads();
+    if (hs_res != 0) {  // (2: ST_FAULT is stored already)
+      if (b == 0 && t == 0) {
+        if (hs_res == 1) st->status = ST_NOTRES;
+        for (int s = 0; s < npiv; ++s) win.made[s] = 0;
+      }
+      return;
+    }
   }
   if (leader) {
     // the flush's record counter; reset write-through and drained before this

@@ -79,6 +79,8 @@ struct State {
   int64_t forced_r;       // >= 0: spx_pivot_at row (norm_kernel)
   int64_t touched_total;  // sum of compacted columns over pivots (bytes)
   int64_t hist_cap;
+  int64_t hs_ticks;       // persistent chains: start-handshake bound (s_memrealtime
+                          // ticks, 100 MHz; < 0 forces ABORT, a test hook)
 };
 
 // Argmin key in memory (partials).  Smallest v, then smallest t; `row`

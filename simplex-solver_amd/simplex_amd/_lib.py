@@ -111,6 +111,9 @@ SIGNATURES = {
     "spx_peer_import": (ctypes.c_int, [_P, ctypes.c_char_p, ctypes.c_int]),
     "spx_peer_chain_local": (ctypes.c_int, [_P]),
     "spx_get_chain_stats": (ctypes.c_int, [_P, _LP]),
+    "spx_set_chain_handshake": (ctypes.c_int, [_P, _I64]),
+    "spx_chain_shm_path": (ctypes.c_int, [ctypes.c_int, ctypes.c_char_p, ctypes.c_int]),
+    "spx_get_chain_reruns": (ctypes.c_int, [_P, _LP]),
     "spx_get_elim_variant": (ctypes.c_int, [_P, _LP]),
     "spx_get_flush_variant": (ctypes.c_int, [_P, _LP]),
     "spx_set_elim_variant": (ctypes.c_int, [_P, ctypes.c_int, ctypes.c_int, ctypes.c_int,

@@ -1,18 +1,25 @@
-"""Row-sharded tableau across GPUs: one process per GPU, RCCL over xGMI.
+"""Row-sharded tableau across GPUs: one process per GPU.
 
-Partitioning: constraint rows 0..m-1 are split into contiguous
-blocks, one per rank; the objective row and the basis are replicated.  Every
-rank chooses the entering column locally (identical objective rows give
-identical choices, no collective).  Per pivot libspx issues ONE RCCL
-all-gather on the context's stream (captured in the pivot-chunk hipGraph):
-each rank contributes [its best (ratio, tie, row) key | that row normalised];
-every rank takes the lexicographic winner (the leaving-row "allreduce-min",
-which RCCL has no MINLOC op for) and the winner's row as the pivot row (the
-owner's broadcast without a host-known root).  Results are bit-identical to
-one GPU.
+Partitioning: constraint rows 0..m-1 are split into contiguous blocks, one per
+rank, tiling 0..m in rank order; the objective row and the basis are
+replicated.  Every rank chooses the entering column locally (identical
+objective rows give identical choices, no collective).  The leaving row is the
+one real exchange of a pivot, and two protocols implement it, bit-identical to
+one GPU and to each other:
 
-torch.distributed is used only to ship the 128-byte RCCL unique id from rank 0
-to the others (any backend: gloo on CPU, nccl on GPU).
+* the row-sharded persistent chain (the default at N > 1, ``enable_peer_chain``):
+  one launch per window on every rank; each block's ratio record is written to
+  every rank's record buffer over xGMI (system-scope granules) and polled
+  locally, and the leaving row's stale values are read from its owner's
+  tableau through a peer pointer (IPC-mapped across processes).  No RCCL call
+  per pivot.
+* the RCCL fallback (``set_chain(1)``): per pivot ONE all-gather of every
+  rank's [best (ratio, tie, row) key | that row normalised]; every rank takes
+  the lexicographic winner (the leaving-row "allreduce-min" RCCL has no MINLOC
+  for) and its row (the owner's broadcast without a host-known root).
+
+torch.distributed only ships small host objects: the 128-byte RCCL unique id
+and the peer chain's IPC blobs (any backend: gloo on CPU).
 """
 from __future__ import annotations
 

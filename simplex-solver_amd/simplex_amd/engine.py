@@ -340,6 +340,21 @@ class DeviceTableau:
         return {"persistent_calls": int(out[0]), "refused_calls": int(out[1]),
                 "blocks_held": int(out[2])}
 
+    def set_chain_handshake(self, us: int = 0) -> None:
+        """Start-handshake bound of persistent chains in us (0: automatic,
+        20 us on one GPU / 100 ms for row shards; < 0: every persistent window
+        aborts and is rerun -- a test hook).  spx_set_chain_handshake."""
+        self._check(self._lib.spx_set_chain_handshake(self._ctx, int(us)),
+                    "spx_set_chain_handshake")
+
+    def chain_reruns(self) -> int:
+        """Windows rerun after their persistent chain found its blocks not
+        co-resident (spx_get_chain_reruns)."""
+        n = ctypes.c_int64()
+        self._check(self._lib.spx_get_chain_reruns(self._ctx, ctypes.byref(n)),
+                    "spx_get_chain_reruns")
+        return int(n.value)
+
     @staticmethod
     def set_chain_budget(device: int, blocks: int) -> None:
         """Process-wide budget of persistent-chain blocks in flight on `device`

@@ -186,6 +186,30 @@ class StorageService:
 
 # --- writing --------------------------------------------------------------
 
+def _read_umask() -> int:
+    """The process umask without changing it: /proc/self/status ('Umask:'),
+    else the os.umask round trip -- done once, at import, before any /solve
+    thread runs (os.umask(0) would briefly open files created meanwhile by
+    other threads to 0666)."""
+    try:
+        with open("/proc/self/status") as f:
+            for line in f:
+                if line.startswith("Umask:"):
+                    return int(line.split()[1], 8)
+    except (OSError, ValueError, IndexError):
+        pass
+    m = os.umask(0o022)
+    os.umask(m)
+    return m
+
+
+_UMASK = _read_umask()
+
+
+def _process_umask() -> int:
+    return _UMASK
+
+
 def _write_atomic(path: str, data: Any) -> None:
     """Stream ``data`` as JSON to a temporary file beside ``path``, then move it
     over ``path`` (a reader sees the empty claim or the whole document)."""
@@ -194,9 +218,7 @@ def _write_atomic(path: str, data: Any) -> None:
     try:
         # mkstemp creates 0600; the report keeps the mode a plain open() gives
         # (0666 & ~umask), as the reference's json.dump target has
-        umask = os.umask(0)
-        os.umask(umask)
-        os.fchmod(fd, 0o666 & ~umask)
+        os.fchmod(fd, 0o666 & ~_process_umask())
         with os.fdopen(fd, "w", encoding="utf-8") as f:
             _dump(data, f, 0)
             f.write("\n")

@@ -12,7 +12,8 @@ HiGHS objective / status / time).  tests/test_gpu_fullsize.py solves the same
 LPs on the GPU through the C-ABI and compares every index, the basis, the
 digests and the objective.
 
-Usage:  python tests/golden/make_fullsize.py [config3|config5|highs3|highs5 ...]
+Usage:  python tests/golden/make_fullsize.py [config3|config5|config5long|highs3|highs5 ...]
+(config5long: the 2^20-pivot digests of config 5, ~1 h on 6 threads, resumable)
 """
 from __future__ import annotations
 
@@ -109,6 +110,62 @@ def oracle_solve(name: str) -> dict:
     return out
 
 
+LONG_PIVOTS = 1 << 20       # the GPU's config-5 run (test_config5_bland_million_pivots_*)
+LONG_CHUNK = 1 << 16        # history digest granularity (localises a divergence)
+LONG_CHECKPOINTS = (1 << 18, 1 << 19, 1 << 20)
+
+
+def hist_digest(h: np.ndarray) -> str:
+    """SHA-256 of a (k, 2) pivot history as little-endian int64 (r, c) pairs."""
+    return hashlib.sha256(np.ascontiguousarray(h, dtype="<i8").tobytes()).hexdigest()
+
+
+def config5_long(scratch: str = "/tmp/spx_config5_long") -> dict:
+    """Config 5 over the 2^20 Bland pivots the GPU test runs: SHA-256 of the
+    tableau at 2^18, 2^19 and 2^20 pivots and of the pivot history in 2^16-pivot
+    chunks (the whole index sequence, 16 digests).  Resumable: the tableau,
+    basis and history are saved to `scratch` (outside the repository) after
+    every chunk, and a restarted run continues from there."""
+    cfg = CONFIGS["config5"]
+    os.makedirs(scratch, exist_ok=True)
+    st_path = os.path.join(scratch, "state.npz")
+    if os.path.exists(st_path):
+        z = np.load(st_path)
+        T, basis, hist = z["T"].copy(), z["basis"].copy(), list(map(tuple, z["hist"].tolist()))
+        cps = json.loads(str(z["cps"]))
+        el0 = float(z["seconds"])
+        print(f"resumed at {len(hist)} pivots", flush=True)
+    else:
+        T, basis = synth.full_tableau(cfg["kind"], cfg["m"], cfg["n"], cfg["seed"])
+        hist, cps, el0 = [], {}, 0.0
+    t0 = time.perf_counter() - el0
+    while len(hist) < LONG_PIVOTS:
+        status, h = C.solve(T, basis, rule=cfg["rule"], max_iters=LONG_CHUNK,
+                            hist_cap=LONG_CHUNK)
+        hist += h
+        if status != 1 or len(h) != LONG_CHUNK:
+            raise RuntimeError(f"config 5 stopped early: status {status} at {len(hist)}")
+        if len(hist) in LONG_CHECKPOINTS:
+            cps[str(len(hist))] = digest(T)
+        el = time.perf_counter() - t0
+        print(f"config5 long: {len(hist)} pivots, {el:.0f} s, z = {T[-1, -1]!r}", flush=True)
+        tmp = os.path.join(scratch, "state.tmp.npz")
+        np.savez(tmp, T=T, basis=basis, hist=np.asarray(hist, dtype=np.int64),
+                 cps=json.dumps(cps), seconds=el)
+        os.replace(tmp, st_path)
+    h = np.asarray(hist, dtype=np.int64).reshape(-1, 2)
+    chunks = [hist_digest(h[i:i + LONG_CHUNK]) for i in range(0, LONG_PIVOTS, LONG_CHUNK)]
+    b0 = np.arange(cfg["n"], cfg["n"] + cfg["m"], dtype=np.int64)
+    out = dict(long_pivots=LONG_PIVOTS, long_chunk=LONG_CHUNK, long_hist_sha256=chunks,
+               long_checkpoint_sha256=cps, long_objective=float(T[-1, -1]),
+               long_basis_sha256=hist_digest(basis.reshape(-1, 1)),
+               long_basis_repeats=zobrist_repeats(h, b0),
+               long_seconds=time.perf_counter() - t0, long_threads=C.threads())
+    print(f"config5 long: done, z = {T[-1, -1]!r}, repeats {out['long_basis_repeats']}",
+          flush=True)
+    return out
+
+
 def _key(r: np.ndarray, v: np.ndarray) -> np.ndarray:
     """Zobrist key of (row, variable): splitmix64 of a packed index."""
     with np.errstate(over="ignore"):
@@ -164,6 +221,9 @@ def main(argv):
         if what.startswith("highs"):
             name = what[5:] if what[5:].startswith("degen") else "config" + what[5:]
             res = highs(name)
+        elif what == "config5long":
+            name = "config5"
+            res = config5_long()
         else:
             name = what
             res = oracle_solve(name)

@@ -4,6 +4,7 @@ launches per pivot.  It must be BYTE-identical to the launch-per-phase chain
 (mode 1) and to the single-pivot engine: pivot sequence, basis, status and the
 tableau (tobytes), and np.array_equal to the CPU oracle.
 """
+import os
 import threading
 
 import numpy as np
@@ -256,6 +257,159 @@ def test_chain_budget_zero_runs_launch_per_phase(eng_cls):
         e.run_pivots(32)
         e.sync()
         assert e.chain_stats()["persistent_calls"] == 1
+
+
+def test_chain_handshake_forced_abort_reruns_bit_exact(eng_cls):
+    """spx_set_chain_handshake(ctx, -1): every persistent window aborts at its
+    start handshake (ST_NOTRES) before any block stores anything; spx_solve,
+    spx_pivot and spx_pivot_at rerun the aborted window with the
+    launch-per-phase chain, so the bytes equal a plain run's and the oracle's.
+    spx_run_pivots cannot rerun: its abort surfaces at spx_state."""
+    from simplex_amd.engine import SpxError
+    T, basis = _random_tableau(300, 900, seed=71)
+    ref = _run(eng_cls, T, basis, 16, 0, max_iters=70)
+    Tc, bc = T.copy(), basis.copy()
+    O.solve_tableau(Tc, bc, max_iters=71)  # the 70 pivots + one rule-chosen pivot
+    nb = set(bc.tolist())
+    fc = next(j for j in range(T.shape[1] - 1) if j not in nb and abs(Tc[5, j]) > 0.05)
+    O.pivot(Tc, 5, fc)
+    bc[5] = fc
+    with eng_cls(0) as e:
+        e.set_window(16)
+        e.load(T, basis)
+        e.set_chain_handshake(-1)
+        res = e.solve(max_iters=70)
+        n0 = e.chain_reruns()
+        assert n0 >= 1 and e.chain_blocks() > 0
+        assert res.iters == ref[0].iters and e.history().tolist() == ref[1]
+        assert e.tableau().tobytes() == ref[2].tobytes()
+        e.pivot()
+        e.pivot_at(5, fc)
+        assert e.chain_reruns() >= n0 + 2
+        assert np.array_equal(e.tableau(), Tc) and np.array_equal(e.basis(), bc)
+        e.run_pivots(16)
+        e.sync()
+        with pytest.raises(SpxError, match="not co-resident"):
+            e.state()
+        e.set_chain_handshake(0)  # automatic bound again: the next call runs persistent
+        e.load(T, basis)
+        r2 = e.solve(max_iters=70)
+        assert r2.iters == 70 and e.history().tolist() == ref[1]
+        assert e.chain_stats()["persistent_calls"] >= 1
+
+
+def test_chain_handshake_more_chains_than_cus_without_admission(eng_cls):
+    """Admission off (budget far above the CU count): six config-3-width chains
+    (6 x 64 blocks > 256 CUs) from six threads.  A chain whose blocks are not
+    all resident aborts at its start handshake before any store and the call
+    reruns the window (launch-per-phase), instead of spinning into a fault:
+    every context byte-identical to a sequential run, no SPX_E_STATE."""
+    T, basis = _random_tableau(257, 16385, seed=63)
+    kw = dict(max_iters=96)
+    ref = _run(eng_cls, T, basis, 24, 0, **kw)
+    assert ref[4] == 64
+    res, reruns, errs = [None] * 6, [0] * 6, []
+    barrier = threading.Barrier(6)
+
+    def work(k):
+        try:
+            with eng_cls(0) as e:
+                e.set_window(24)
+                e.load(T, basis)
+                barrier.wait()
+                for _ in range(2):
+                    e.solve(max_iters=48)
+                res[k] = (e.history().tolist(), e.tableau().tobytes())
+                reruns[k] = e.chain_reruns()
+        except Exception as ex:  # noqa: BLE001 - reported below
+            errs.append(repr(ex))
+
+    eng_cls.set_chain_budget(0, 100000)
+    try:
+        th = [threading.Thread(target=work, args=(k,)) for k in range(6)]
+        for x in th:
+            x.start()
+        for x in th:
+            x.join()
+    finally:
+        eng_cls.set_chain_budget(0, -1)
+    assert not errs, errs
+    for r in res:
+        assert r[0] == ref[1] and r[1] == ref[2].tobytes()
+    print(f"windows rerun after a start-handshake abort: {sum(reruns)} ({reruns})")
+
+
+def _shm_entries(path):
+    import fcntl
+    import struct
+    try:
+        with open(path, "rb") as f:
+            fcntl.flock(f, fcntl.LOCK_SH)
+            raw = f.read(512)
+    except FileNotFoundError:
+        return []
+    raw = raw.ljust(512, b"\0")
+    return [struct.unpack_from("<ii", raw, 8 * x) for x in range(64)]
+
+
+def _shm_put(path, pid, blocks):
+    """Write an entry {pid, blocks} into a free slot of the admission table,
+    under its flock (as another process's libspx would)."""
+    import fcntl
+    import struct
+    fd = os.open(path, os.O_RDWR | os.O_CREAT, 0o666)
+    try:
+        fcntl.flock(fd, fcntl.LOCK_EX)
+        raw = os.pread(fd, 512, 0).ljust(512, b"\0")
+        ent = [struct.unpack_from("<ii", raw, 8 * x) for x in range(64)]
+        slot = next(x for x, (p, b) in enumerate(ent) if p <= 0 or b <= 0)
+        os.pwrite(fd, struct.pack("<ii", pid, blocks), 8 * slot)
+        fcntl.flock(fd, fcntl.LOCK_UN)
+    finally:
+        os.close(fd)
+
+
+def test_chain_admission_shared_across_processes(eng_cls):
+    """The admission budget is shared by the processes on a GPU through
+    /dev/shm/spx_chain_<bus id> (the reference runs gunicorn with 2 workers,
+    /root/reference/dockerfile:34).  With another live process holding all but
+    56 of the CUs' blocks, a 64-block chain is refused (launch-per-phase, same
+    bytes); once that process is gone its entry is free and the chain is
+    admitted; after spx_destroy (no explicit sync) this process's entry is 0."""
+    import ctypes
+    import subprocess
+    import torch
+    from simplex_amd import _lib
+    buf = ctypes.create_string_buffer(256)
+    assert _lib.lib().spx_chain_shm_path(0, buf, 256) == 0
+    path = buf.value.decode()
+    assert path.startswith("/dev/shm/spx_chain_")
+    n_cu = torch.cuda.get_device_properties(0).multi_processor_count
+    T, basis = _random_tableau(65, 16385, seed=64)  # config-3 width: 64 chain blocks
+    ref = _run(eng_cls, T, basis, 24, 0, max_iters=48)
+    assert ref[4] == 64
+    other = subprocess.Popen(["sleep", "300"])
+    try:
+        _shm_put(path, other.pid, n_cu - 56)
+        with eng_cls(0) as e:
+            e.set_window(24)
+            e.load(T, basis)
+            e.solve(max_iters=48)
+            st = e.chain_stats()
+            assert st["refused_calls"] == 1 and st["persistent_calls"] == 0, st
+            assert e.history().tolist() == ref[1] and e.tableau().tobytes() == ref[2].tobytes()
+            other.kill()
+            other.wait()
+            e.load(T, basis)
+            e.solve(max_iters=48)
+            assert e.chain_stats()["persistent_calls"] == 1
+            assert not any(p == other.pid and b > 0 for p, b in _shm_entries(path))
+            e.run_pivots(4 * 24)  # no sync: released behind the launches, or at destroy
+        assert not any(p == os.getpid() and b > 0 for p, b in _shm_entries(path))
+    finally:
+        if other.poll() is None:
+            other.kill()
+            other.wait()
 
 
 def test_chain_set_validated(eng_cls):

@@ -98,26 +98,48 @@ def test_degenerate_bland_to_optimality_pinned(name):
     assert fx["basis_repeats"] == 0
 
 
-def test_config5_bland_million_pivots_no_basis_repeats():
-    """Anti-cycling at full size: 2^20 Bland pivots of config 5 on the GPU
-    (K = 24) revisit no basis (Zobrist hashes of every basis along the
-    recorded history), and their first 100,000 are the oracle's."""
+def test_config5_bland_million_pivots_pinned():
+    """Config 5 over the 2^20 Bland pivots the GPU runs (K = 24): every index
+    of the run against the C oracle's -- SHA-256 digests of the (r, c)
+    sequence in 2^16-pivot chunks --, the tableau digests at 2^18, 2^19 and
+    2^20 pivots, the final basis, and no basis revisited (Zobrist hashes of
+    every basis along the run; the detector itself is checked on Beale's
+    cycling LP in the CPU suite).  Fixture: make_fullsize.py config5long."""
     from simplex_amd import synth
     from simplex_amd.engine import DeviceTableau
     import sys
     sys.path.insert(0, GOLD)
     from make_fullsize import zobrist_repeats
     fx, hist, _ = _fixture("config5")
+    if "long_hist_sha256" not in fx:
+        pytest.skip("config5long fixture not generated")
     T, basis = synth.full_tableau("degenerate", 4096, 4096, 5)
+    n, chunk = fx["long_pivots"], fx["long_chunk"]
+    cps = {int(k): v for k, v in fx["long_checkpoint_sha256"].items()}
     with DeviceTableau(0) as e:
         e.set_window(24)
         e.load(T, basis)
         del T
-        r = e.solve(rule="bland", max_iters=1 << 20)
-        assert r.status == 1 and r.iters == 1 << 20
+        done = 0
+        for k in sorted(cps):
+            r = e.solve(rule="bland", max_iters=k - done)
+            assert r.status == 1 and r.iters == k - done
+            done = k
+            assert _digest(e.tableau()) == cps[k], f"tableau after {k} pivots"
+        assert done == n
         h = e.history()
+        b = e.basis()
+        z = e.state()[2]
+    assert len(h) == n
     assert np.array_equal(h[:len(hist)], hist)
-    assert zobrist_repeats(h, basis) == 0
+    for x, want in enumerate(fx["long_hist_sha256"]):
+        got = hashlib.sha256(np.ascontiguousarray(h[x * chunk:(x + 1) * chunk],
+                                                  dtype="<i8").tobytes()).hexdigest()
+        assert got == want, f"pivots {x * chunk}..{(x + 1) * chunk - 1} differ from the oracle's"
+    assert hashlib.sha256(np.ascontiguousarray(b.reshape(-1, 1), dtype="<i8").tobytes()
+                          ).hexdigest() == fx["long_basis_sha256"]
+    assert z == fx["long_objective"]
+    assert zobrist_repeats(h, basis) == 0 == fx["long_basis_repeats"]
 
 
 @pytest.mark.parametrize("window", [24, 28])

@@ -45,7 +45,8 @@ def _peer_threads(world, kind, m, n, seed, rule, K, peer=True, mode=0, **solve_k
                     s.enable_peer_chain()
                 blocks = s.chain_blocks()
                 res = s.solve(rule=rule, **solve_kw)
-                outs[rank] = (r0, r1, res, s.history().tolist(), s.tableau(), s.basis(), blocks)
+                outs[rank] = (r0, r1, res, s.history().tolist(), s.tableau(), s.basis(), blocks,
+                              s.chain_reruns())
         except Exception as ex:  # pragma: no cover
             errors.append(ex)
 
@@ -62,7 +63,7 @@ def _check_vs_oracle(outs, kind, m, n, seed, rule, max_iters=200000):
     from simplex_amd import synth
     T, basis = synth.full_tableau(kind, m, n, seed)
     st, hist = O.solve_tableau(T, basis, rule=rule, max_iters=max_iters)
-    for rank, (r0, r1, res, h, Tl, b, blocks) in outs.items():
+    for rank, (r0, r1, res, h, Tl, b, *_) in outs.items():
         assert res.status == st
         assert [tuple(x) for x in h] == hist
         assert np.array_equal(Tl[:-1], T[r0:r1])
@@ -79,20 +80,18 @@ def _check_vs_oracle(outs, kind, m, n, seed, rule, max_iters=200000):
     (2, "degenerate", 64, 64, "bland", 12),
     (3, "degenerate", 96, 96, "bland", 32),
     (3, "dense", 7, 9, "dantzig", 4),   # ranks with two or three rows
-    (4, "dense", 7, 9, "dantzig", 4),   # >= 4 virtual ranks: launch-per-phase (see below)
+    (4, "dense", 7, 9, "dantzig", 4),   # 4-5 ranks: streams may share a hardware queue
     (5, "dense", 7, 9, "dantzig", 4),
 ])
 def test_peer_chain_virtual_ranks_bit_exact(world, kind, m, n, rule, K):
     """Virtual ranks are streams of one process, which get GPU_MAX_HW_QUEUES
-    (4) hardware queues: two chains on one queue would run one after the
-    other and wait for each other's records, so with one queue kept for the
-    process's other streams, 4 or more virtual ranks on a GPU take the
-    launch-per-phase path (chain_blocks 0), same bytes."""
+    (4) hardware queues: two ranks' chains on one queue run one after the
+    other.  The start handshake (chain_start) turns that into an abort of the
+    window on every rank before any store, and the calls rerun it with the
+    launch-per-phase path: same bytes whichever way each window ran."""
     outs = _peer_threads(world, kind, m, n, 3, rule, K)
-    if world <= 3:
-        assert all(o[6] >= 1 for o in outs.values()), "the persistent sharded chain did not run"
-    else:
-        assert all(o[6] == 0 for o in outs.values())
+    assert all(o[6] >= 1 for o in outs.values()), "the persistent sharded chain was not set up"
+    assert len({o[7] for o in outs.values()}) == 1, "ranks disagree on the windows rerun"
     _check_vs_oracle(outs, kind, m, n, 3, rule)
 
 
@@ -109,6 +108,99 @@ def test_peer_chain_config3_width(world, K):
     for r in range(world):
         assert outs[r][3] == lazy[r][3] and outs[r][4].tobytes() == lazy[r][4].tobytes()
     _check_vs_oracle(outs, "dense", m, n, 9, "dantzig", max_iters=5 * K + 7)
+
+
+def test_peer_chain_uneven_split_more_rows_than_the_even_share():
+    """Row blocks of 600 / 100 / 100 rows of an 800-row tableau with only 301
+    columns: the chain grid must come from the LARGEST block (rank 0's 600
+    rows need 3 blocks of 256 threads; the even share, 267 rows, would give 2,
+    and rows 256..299 of each of rank 0's blocks would own no thread).  Every
+    rank agrees on the grid at spx_peer_chain_local; bit-exact vs the oracle."""
+    from simplex_amd import dist
+    rng = np.random.default_rng(17)
+    m, N, K, world = 800, 301, 8, 3
+    T = np.zeros((m + 1, N))
+    T[:m, :-1] = rng.uniform(0.05, 1.0, size=(m, N - 1))
+    T[:m, -1] = rng.uniform(1.0, 2.0, size=m) * 50
+    T[m, :-1] = -rng.uniform(0.1, 1.0, size=N - 1)
+    basis = np.arange(N, N + m, dtype=np.int64)
+    splits = [(0, 600), (600, 700), (700, 800)]
+    uid = b"uneven" + os.urandom(122)
+    outs, errors = {}, []
+
+    def rank_main(rank):
+        try:
+            r0, r1 = splits[rank]
+            with dist.ShardedTableau(0, rank, world, uid, local=True) as s:
+                s.set_window(K)
+                s.load_rows(np.asfortranarray(T[r0:r1]), T[m], basis, m, r0)
+                s.enable_peer_chain()
+                outs[rank] = (r0, r1, s.chain_blocks(), s.solve(max_iters=60),
+                              s.history().tolist(), s.tableau(), s.basis())
+        except Exception as ex:  # pragma: no cover
+            errors.append(ex)
+
+    th = [threading.Thread(target=rank_main, args=(r,)) for r in range(world)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=300)
+    assert not errors, errors
+    Tc, bc = T.copy(), basis.copy()
+    st, hist = O.solve_tableau(Tc, bc, max_iters=60)
+    for rank, (r0, r1, blocks, res, h, Tl, b) in outs.items():
+        assert blocks == 3, blocks
+        assert res.status == st and [tuple(x) for x in h] == hist
+        assert np.array_equal(Tl[:-1], Tc[r0:r1]) and np.array_equal(Tl[-1], Tc[-1])
+        assert np.array_equal(b, bc)
+
+
+def test_peer_chain_streams_interleaved_on_hardware_queues():
+    """Three virtual ranks whose contexts are created with three other streams
+    between each (the creation order that maps two ranks' streams onto one of
+    the process's 4 hardware queues): a rank's chain then waits in its start
+    handshake for blocks queued behind another rank's chain.  The window aborts
+    on every rank before any store and is rerun (launch-per-phase); the solve
+    must end bit-exact vs the oracle, with no SPX_E_STATE."""
+    from simplex_amd import dist, synth
+    from simplex_amd.engine import DeviceTableau
+    m, n, K, world, seed = 300, 500, 8, 3, 21
+    uid = b"queues" + os.urandom(122)
+    ctxs, spare = [], []
+    try:
+        for rank in range(world):
+            ctxs.append(dist.ShardedTableau(0, rank, world, uid, local=True))
+            for _ in range(3):  # three more streams, each used once
+                d = DeviceTableau(0)
+                d.load(np.ones((2, 3)), np.array([1], dtype=np.int64))
+                spare.append(d)
+        outs, errors = {}, []
+
+        def rank_main(rank):
+            try:
+                s = ctxs[rank]
+                r0, r1 = dist.row_partition(m, world, rank)
+                T, obj, basis = synth.tableau_rows("dense", m, n, seed, r0, r1, order="F")
+                s.set_window(K)
+                s.load_shard(T, obj, basis, m, r0)
+                s.enable_peer_chain()
+                res = s.solve()
+                outs[rank] = (r0, r1, res, s.history().tolist(), s.tableau(), s.basis(),
+                              s.chain_blocks(), s.chain_reruns())
+            except Exception as ex:  # pragma: no cover
+                errors.append(ex)
+
+        th = [threading.Thread(target=rank_main, args=(r,)) for r in range(world)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join(timeout=300)
+        assert not errors, errors
+    finally:
+        for x in ctxs + spare:
+            x.close()
+    _check_vs_oracle(outs, "dense", m, n, seed, "dantzig")
+    print("windows rerun per rank:", [outs[r][7] for r in range(world)])
 
 
 def test_peer_chain_mode1_falls_back_to_lazy():
@@ -198,3 +290,40 @@ def test_peer_chain_two_processes_ipc(args):
     p = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=280)
     out = p.stdout + p.stderr
     assert p.returncode == 0 and "RCCL_RANKS_CHECK PASS" in out, out[-4000:]
+
+
+@pytest.mark.timeout(400)
+def test_bench_same_device_two_ranks():
+    """bench.py's N > 1 path end to end on ONE GPU (--same-device: two
+    processes on GPU 0, peer-only shards over IPC, no RCCL): the peer self-test
+    against the single-GPU path, the barrier-bracketed timed region, the
+    max-over-ranks time and the rank-0 JSON line.  The line must say n_gpus 2,
+    config 4, the peer chain enabled, carry the shard flush's roofline, and its
+    pivot sequence (every pivot of the run from the slack basis) must be the
+    oracle's: the prefix of the config-3 full-solve fixture."""
+    import hashlib
+    import json
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", HSA_ENABLE_IPC_MODE_LEGACY="0")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.join(ROOT, "bench.py"), "--gpus", "2", "--same-device", "--steps", "4",
+           "--warmup", "1", "--cpu-seconds", "0"]
+    p = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=380)
+    out = p.stdout + p.stderr
+    assert p.returncode == 0, out[-4000:]
+    lines = [x for x in p.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1, out[-4000:]
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == 2 and line["steps"] == 4
+    assert line["config"]["workload"].startswith("config 4")
+    assert line["config"]["same_device"] is True
+    assert line["config"]["peer_chain"]["enabled"] is True, line["config"]["peer_chain"]
+    assert line["config"]["chain_blocks"] == 64
+    rf = line["roofline"]
+    assert rf["kernel"] == "spx::flush_lds_kernel" and 0 < rf["frac"] < 1.0
+    assert line["pivots_timed"] == 4 * 24 and line["value"] > 0
+    z = np.load(os.path.join(ROOT, "tests", "golden", "fullsize_config3.npz"))
+    k = line["pivots_total"]
+    assert 5 * 24 <= k <= len(z["hist"])
+    want = hashlib.sha256(np.ascontiguousarray(z["hist"][:k], dtype="<i8").tobytes()).hexdigest()
+    assert line["pivots_sha256"] == want, "the sharded run's pivots differ from the oracle's"

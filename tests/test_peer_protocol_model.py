@@ -1,0 +1,177 @@
+"""CPU tests of the row-sharded persistent chain's cross-rank protocol
+(tests/peer_protocol_model.py restates chain_shard_kernel + chain_start with a
+thread per block and shared tagged granules).
+
+The model must reproduce the oracle bit for bit under delays injected where
+the GPU's timing varies (records published late, polls late, a rank running a
+slot ahead), stop every rank at the same pivot on rank 0's stop bit, and rerun
+a window whose start handshake aborted.  Two mutants show the protocol's
+guards are load-bearing: one record half instead of two (by pivot parity)
+deadlocks when a rank runs a slot ahead, and no window-end barrier lets a
+rank's flush rewrite a row a peer is still gathering.
+"""
+import random
+import threading
+
+import numpy as np
+import pytest
+
+import peer_protocol_model as M
+from oracle import simplex_oracle as O
+
+
+def _run(world=2, B=2, kind="dense", m=20, n=14, seed=3, K=4, rule="dantzig", mutant=(),
+         delay=None, late=None, max_iters=10 ** 6, hs_bound=0.5, stop_after=None):
+    from simplex_amd import synth
+    from simplex_amd.dist import row_partition
+    dev = M.Device(world, B, mutant)
+    ranks = []
+    for r in range(world):
+        r0, r1 = row_partition(m, world, r)
+        T, obj, basis = synth.tableau_rows(kind, m, n, seed, r0, r1, order="C")
+        ranks.append(M.Rank(dev, r, T, obj, basis, r0, K, rule, delay=delay, late=late,
+                            hs_bound=hs_bound))
+    errs, res = [], {}
+
+    def go(rk):
+        try:
+            res[rk.rank] = rk.solve(max_iters)
+        except Exception as ex:  # noqa: BLE001
+            errs.append(ex)
+
+    th = [threading.Thread(target=go, args=(rk,)) for rk in ranks]
+    for t in th:
+        t.start()
+    if stop_after is not None:
+        threading.Timer(stop_after, ranks[0].stop.set).start()
+    for t in th:
+        t.join()
+    return ranks, res, errs
+
+
+def _oracle(kind, m, n, seed, rule, max_iters=10 ** 6):
+    from simplex_amd import synth
+    T, basis = synth.full_tableau(kind, m, n, seed)
+    st, hist = O.solve_tableau(T, basis, rule=rule, max_iters=max_iters)
+    return st, hist, T, basis
+
+
+def _check(ranks, res, kind, m, n, seed, rule, max_iters=10 ** 6):
+    st, hist, T, basis = _oracle(kind, m, n, seed, rule, max_iters)
+    for rk in ranks:
+        assert res[rk.rank] == st
+        assert rk.hist == hist
+        r0 = rk.row0
+        assert np.array_equal(rk.A, T[r0:r0 + rk.m_local])
+        assert np.array_equal(rk.obj, T[-1])
+        assert np.array_equal(rk.basis, basis)
+
+
+def _jitter(seed, scale=2e-4):
+    rng = random.Random(seed)
+    lock = threading.Lock()
+
+    def delay(*_):
+        with lock:
+            x = rng.random()
+        if x < 0.3:
+            import time
+            time.sleep(x * scale / 0.3)
+    return delay
+
+
+@pytest.mark.parametrize("world,B,kind,m,n,K,rule", [
+    (2, 2, "dense", 20, 14, 4, "dantzig"),
+    (3, 2, "dense", 21, 16, 3, "dantzig"),
+    (2, 3, "dense", 30, 25, 8, "dantzig"),
+    (2, 2, "degenerate", 16, 16, 4, "bland"),
+    (3, 3, "degenerate", 18, 18, 5, "bland"),
+])
+def test_model_matches_oracle_under_jitter(world, B, kind, m, n, K, rule):
+    ranks, res, errs = _run(world, B, kind, m, n, 5, K, rule, delay=_jitter(world * 7 + K))
+    assert not errs, errs
+    _check(ranks, res, kind, m, n, 5, rule)
+
+
+def test_model_rank_a_slot_ahead_is_safe_with_two_halves():
+    """Rank 1 polls the ratio records late at every slot, so rank 0 publishes
+    pivot q+1's records (into rank 1's buffer too) before rank 1 read pivot
+    q's: the parity halves keep them apart."""
+    import time
+
+    def delay(point, rank, b, q, *rest):
+        if point == "poll_ratio" and rank == 1:
+            time.sleep(0.01)
+    ranks, res, errs = _run(delay=delay)
+    assert not errs, errs
+    _check(ranks, res, "dense", 20, 14, 3, "dantzig")
+
+
+def test_model_mutant_one_record_half_deadlocks():
+    """The same schedule with ONE record buffer: rank 0's pivot-(q+1) records
+    overwrite its pivot-q records in rank 1's buffer before rank 1 polled them,
+    and rank 1's poll never matches (the kernels' ST_FAULT)."""
+    import time
+
+    def delay(point, rank, b, q, *rest):
+        if point == "poll_ratio" and rank == 1 and q == 1:
+            time.sleep(0.05)
+    old = M.WAIT_LIMIT
+    M.WAIT_LIMIT = 0.5
+    try:
+        _, _, errs = _run(delay=delay, mutant=("one_half",), max_iters=8)
+    finally:
+        M.WAIT_LIMIT = old
+    assert errs and all(isinstance(e, M.Timeout) for e in errs), errs
+
+
+def test_model_mutant_no_window_end_barrier_corrupts():
+    """In the last slot of a window, a rank gathers the leaving row from its
+    peer's rows late.  With the window-end barrier the owner's flush waits for
+    it; without it the owner rewrites that row first and the late rank
+    computes p from post-flush values."""
+    import time
+
+    K, m, n = 4, 40, 30
+
+    def delay(point, rank, b, q, *rest):
+        if point == "gather_row" and q == K - 1 and rest and rest[0] != rank:
+            time.sleep(0.03)
+    ranks, res, errs = _run(delay=delay, K=K, m=m, n=n)
+    assert not errs, errs
+    _check(ranks, res, "dense", m, n, 3, "dantzig")
+    ranks, res, errs = _run(delay=delay, K=K, m=m, n=n, mutant=("no_done_barrier",))
+    st, hist, T, basis = _oracle("dense", m, n, 3, "dantzig")
+    broken = bool(errs) or any(rk.hist != hist or not np.array_equal(rk.A, T[rk.row0:rk.row0 + rk.m_local])
+                               for rk in ranks)
+    assert broken, "the no-barrier mutant reproduced the oracle: the schedule missed the hazard"
+
+
+def test_model_stop_bit_stops_every_rank_at_the_same_pivot():
+    """Rank 0's stop request rides in its ratio records: every rank stops
+    before the same pivot, with the oracle's prefix."""
+    import time
+
+    def delay(*_):
+        time.sleep(0.002)
+    ranks, res, errs = _run(m=40, n=30, K=3, delay=delay, stop_after=0.05)
+    assert not errs, errs
+    its = {rk.it for rk in ranks}
+    assert len(its) == 1
+    k = its.pop()
+    assert all(res[rk.rank] in (0, 1) for rk in ranks)
+    _, hist, T, basis = _oracle("dense", 40, 30, 3, "dantzig", max_iters=k)
+    for rk in ranks:
+        assert rk.hist == hist
+        assert np.array_equal(rk.A, T[rk.row0:rk.row0 + rk.m_local])
+
+
+def test_model_start_handshake_late_block_aborts_then_reruns():
+    """A block of rank 1 starts window 1 after the handshake bound: every
+    block of every rank reads the same ABORT verdict, nothing is stored, each
+    host reruns the window with the next epoch, and the solve is exact."""
+    ranks, res, errs = _run(late=lambda W, b: 0.2 if W == 1 and b == 1 else 0.0,
+                            hs_bound=0.05)
+    assert not errs, errs
+    assert all(rk.reruns >= 1 for rk in ranks)
+    _check(ranks, res, "dense", 20, 14, 3, "dantzig")

@@ -1,0 +1,27 @@
+#!/bin/bash
+# Round-4 GPU steps: STEPS="probe tests bench ..." (each under its own time
+# limit; stops at the first failure, GPU fault or time limit).
+set -u
+cd "${GRAFT_REPO_ROOT}"; export TMPDIR=/tmp
+O=gpurun_out/${OUT:-r04}; mkdir -p $O
+run() { local lim=$1 log=$2; shift 2
+  timeout -k 10 "$lim" "$@" > "$O/$log" 2>&1
+  local rc=$?; echo "[$log] rc=$rc"; tail -${TAILN:-4} "$O/$log" | cut -c1-600
+  [ $rc != 0 ] && exit $rc; return 0; }
+PYT="python -u -m pytest -x -v --timeout 300 --timeout-method thread"
+for s in ${STEPS:-probe tests bench}; do
+  case $s in
+    probe) TAILN=12 run 120 xcd_probe.log ./tools/xcd_exchange_probe 2000 ;;
+    tests) run 900 pytest_sel.log $PYT ${TESTS:-tests/test_gpu_chain.py tests/test_gpu_peer_chain.py} ;;
+    suite) run 1100 pytest_gpu.log $PYT -m gpu tests ;;
+    bench) TAILN=1 run 300 bench_driver.log python bench.py --steps 20 --warmup 5 --cpu-seconds 0 ;;
+    bench40) TAILN=1 run 300 bench40.log python bench.py --steps 40 --warmup 5 --cpu-seconds 0 ;;
+    benchcpu) TAILN=1 run 400 bench_cpu.log python bench.py --cpu-seconds 15 ;;
+    same) TAILN=1 run 400 bench_same.log python -m torch.distributed.run --nnodes=1 --nproc-per-node=2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --same-device --steps 20 --warmup 5 --cpu-seconds 0 ;;
+    phases) TAILN=30 run 200 phases24.log python tools/probe_phases.py --window 24 ;;
+    smoke) run 200 smoke.log python -c "import __graft_entry__ as g; g.smoke()" ;;
+    rocprof) run 400 rocprof.log rocprofv3 --kernel-trace --stats -d $O/prof -o bench --output-format csv -- python3 bench.py --steps 20 --warmup 5 --cpu-seconds 0 ;;
+    *) echo "unknown step $s"; exit 3 ;;
+  esac
+done
+exit 0
