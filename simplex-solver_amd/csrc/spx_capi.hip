@@ -261,6 +261,7 @@ int free_buffers(spx_ctx* ctx) {
   dfree(ctx->win.epoch);
   dfree(ctx->win.nlist);
   dfree(ctx->win.rec);
+  dfree(ctx->win.xcnt);
   dfree(ctx->gr_enter);
   dfree(ctx->gr_ratio);
   ctx->loaded = false;
@@ -465,7 +466,27 @@ int64_t chain_need(int64_t N, int64_t rows, int cb, int min_blocks) {
 // refused admission, or a tableau wider than CB x CUs columns).  Row shards
 // take the geometry every rank agreed on at spx_peer_import /
 // spx_peer_chain_local (shard_geometry), so no rank decides alone.
-int chain_blocks(spx_ctx* ctx, int* cb_out = nullptr, bool ignore_admission = false) {
+// The one-XCD chain (chain_xcd_kernel, mode 4): B blocks of 512 threads on one
+// XCD, each owning <= 512 columns and <= 256 rows, the window histories in LDS
+// (K <= 24).  Returns B, or 0 when the tableau or the window does not fit.
+int chain_xcd_blocks(const spx_ctx* ctx) {
+  if (ctx->sharded || ctx->win_k > 24) return 0;
+  const int per_xcd = std::max(1, ctx->n_cu / 8);
+  const int64_t need = std::max<int64_t>({(ctx->N - 1 + 511) / 512, (ctx->m_local + 255) / 256,
+                                          1, (int64_t)ctx->chain_min_blocks});
+  return need <= per_xcd && need <= 64 ? (int)need : 0;
+}
+
+// Persistent chain geometry: B blocks of CB threads (one per CU, all
+// resident), each owning <= CB columns and <= CB rows.  Returns B (and CB in
+// *cb, whether it is the one-XCD chain in *xcd), or 0 when the chain does not
+// apply (the launch-per-phase mode, a refused admission, or a tableau wider
+// than CB x CUs columns).  Row shards take the geometry every rank agreed on
+// at spx_peer_import / spx_peer_chain_local (shard_geometry), so no rank
+// decides alone.
+int chain_blocks(spx_ctx* ctx, int* cb_out = nullptr, bool ignore_admission = false,
+                 bool* xcd_out = nullptr) {
+  if (xcd_out) *xcd_out = false;
   if (ctx->chain_mode == 1) return 0;
   if (ctx->sharded) {  // shards: only once the peers are known
     if (!ctx->peer_ok) return 0;
@@ -474,6 +495,14 @@ int chain_blocks(spx_ctx* ctx, int* cb_out = nullptr, bool ignore_admission = fa
   }
   if (ctx->chain_denied && !ignore_admission) return 0;
   if (!ctx->n_cu) ctx->n_cu = device_cus(ctx->device);
+  if (ctx->chain_mode == 4) {  // the one-XCD chain where it fits, else the spread one
+    const int bx = chain_xcd_blocks(ctx);
+    if (bx > 0) {
+      if (cb_out) *cb_out = 512;
+      if (xcd_out) *xcd_out = true;
+      return bx;
+    }
+  }
   const int cb = chain_cb(ctx->chain_mode, std::max<int64_t>(ctx->N, ctx->m_local), ctx->n_cu);
   if (cb_out) *cb_out = cb;
   const int64_t need = chain_need(ctx->N, ctx->m_local, cb, ctx->chain_min_blocks);
@@ -685,14 +714,26 @@ template <int KMAX>
 int enqueue_window_t(spx_ctx* ctx, int npiv, bool time_flush) {
   const int nbw = lazy_ratio_grid(ctx);
   int cb = BLK;
-  const int B = chain_blocks(ctx, &cb);
+  bool xcd = false;
+  const int B = chain_blocks(ctx, &cb, false, &xcd);
   std::pair<hipEvent_t, hipEvent_t>* ec = nullptr;
   if (ctx->time_chain) {
     int rc = next_event_pair(ctx, ctx->evc, ctx->evc_used, &ec);
     if (!rc) rc = record_event(ctx, ec->first);
     if (rc) return rc;
   }
-  if (B > 0) {
+  if (B > 0 && xcd) {
+    // one 512-thread block per CU; the first XCD to gather B of them runs the chain
+    const int cpb = (int)((ctx->N - 1 + B - 1) / B);
+    const int rpb = (int)std::max<int64_t>(1, (ctx->m_local + B - 1) / B);
+    if constexpr (KMAX <= 24) {
+      hipLaunchKernelGGL(chain_xcd_kernel<KMAX>, dim3(ctx->n_cu), dim3(512), 0, ctx->stream,
+                         ctx->enter_part, ctx->st, (const Params*)ctx->prm,
+                         std::max(NWAVE * ctx->nbn, B), (const double*)ctx->A, ctx->ld,
+                         ctx->m_local, ctx->N, ctx->obj, ctx->win, npiv, ctx->basis, ctx->hist,
+                         ctx->gr_enter, ctx->gr_ratio, cpb, rpb, B);
+    }
+  } else if (B > 0) {
     const int cpb = (int)((ctx->N - 1 + B - 1) / B);  // (B * cpb == N-1: xown owns the RHS)
     const int rpb = (int)std::max<int64_t>(1, (ctx->m_local + B - 1) / B);
     auto kern = ctx->sharded ? (cb == 512 ? chain_shard_kernel<KMAX, 512>
@@ -1030,6 +1071,8 @@ int alloc_common(spx_ctx* ctx, int64_t m_local, int64_t N, int64_t m_global, int
     HIPC(hipMalloc(&ctx->win.epoch, sizeof(uint32_t)));
     HIPC(hipMalloc(&ctx->win.nlist, sizeof(int32_t)));
     HIPC(hipMalloc(&ctx->win.rec, sizeof(double) * RECW * N));
+    HIPC(hipMalloc(&ctx->win.xcnt, sizeof(uint32_t) * 9));
+    HIPC(hipMemsetAsync(ctx->win.xcnt, 0, sizeof(uint32_t) * 9, ctx->stream));
     HIPC(hipMemsetAsync(ctx->win.nlist, 0, sizeof(int32_t), ctx->stream));
     HIPC(hipMemsetAsync(ctx->win.rec, 0, sizeof(double) * RECW * N, ctx->stream));
     HIPC(hipMemsetAsync(ctx->win.F, 0, sizeof(double) * KW * ctx->ld, ctx->stream));
@@ -1988,8 +2031,8 @@ int spx_get_elim_variant(const spx_ctx* ctx, int64_t out[7]) {
 // its minimum (tuning; 0 = minimum).
 int spx_set_chain(spx_ctx* ctx, int mode, int min_blocks) {
   if (!ctx) return SPX_E_ARG;
-  CHECK_ARG(mode >= 0 && mode <= 3 && min_blocks >= 0 && min_blocks <= CHAIN_MAX_BLOCKS,
-            "chain mode must be 0..3, min_blocks 0..256");
+  CHECK_ARG(mode >= 0 && mode <= 4 && min_blocks >= 0 && min_blocks <= CHAIN_MAX_BLOCKS,
+            "chain mode must be 0..4, min_blocks 0..256");
   ctx->chain_mode = mode;
   ctx->chain_min_blocks = min_blocks;
   drop_graphs(ctx);

@@ -93,6 +93,8 @@ struct Window {
   int32_t* nlist;    // 1             : records in `rec` (reset by lazy_ratio slot 0)
   double* rec;       // N x RECW      : the window's touched columns, compacted by the
                      //                 last lazy_norm: [j | path flags, pad, p_0 .. p_{K-1}]
+  uint32_t* xcnt;    // 9             : the one-XCD chain's per-XCD tickets + the chosen XCD
+                     //                 (spx_chain.hpp chain_xcd_kernel; zeroed by row_fix)
 };
 constexpr int RECW = KW + 2;  // doubles per record (272 B)
 
@@ -814,6 +816,9 @@ __global__ __launch_bounds__(BLK) void row_fix_kernel(double* __restrict__ A, in
   __shared__ int lastL[K];
   // one thread per record of the window (the flush's compacted list: column,
   // path flags, p_0..p_{K-1}); all loads are independent: issue them together
+  // the next window's one-XCD chain starts from zeroed tickets (every launch of
+  // this window's chain -- its late blocks included -- has ended: stream order)
+  if (blockIdx.x == 0 && threadIdx.x < 9) win.xcnt[threadIdx.x] = 0u;
   const int kr = blockIdx.x * BLK + threadIdx.x;
   const bool live = kr < *win.nlist;
   const int64_t hdr = reinterpret_cast<const int64_t*>(win.rec)[(int64_t)(live ? kr : 0) * RECW];

@@ -48,7 +48,7 @@ def _run(eng_cls, T, basis, K, mode, min_blocks=0, **kw):
 @pytest.mark.parametrize("K", [2, 8, 16, 24, 28, 32])
 @pytest.mark.parametrize("shape", [(2, 3), (17, 40), (300, 700), (1025, 2051)])
 @pytest.mark.parametrize("rule", ["dantzig", "bland"])
-@pytest.mark.parametrize("mode", [2, 3], ids=["cb256", "cb512"])
+@pytest.mark.parametrize("mode", [2, 3, 4], ids=["cb256", "cb512", "xcd"])
 def test_chain_matches_lazy_chain_and_oracle(eng_cls, K, shape, rule, mode):
     T, basis = _random_tableau(*shape, seed=shape[0] * 7 + K)
     kw = dict(max_iters=3 * K + 5, rule=rule)
@@ -95,6 +95,36 @@ def test_chain_grid_sizes_bit_exact(eng_cls, min_blocks, mode):
     assert h == h1 and res.iters == res1.iters and out.tobytes() == out1.tobytes()
 
 
+@pytest.mark.parametrize("min_blocks", [0, 3, 17, 32])
+def test_chain_xcd_grid_sizes_bit_exact(eng_cls, min_blocks):
+    """The one-XCD chain (mode 4) with more blocks than the minimum, up to a
+    whole XCD's 32: the same bytes as the launch-per-phase chain and the
+    oracle; past 32 blocks (or K > 24, or a tableau wider than 32 x 512
+    columns) mode 4 runs the spread chain."""
+    T, basis = _random_tableau(700, 2100, seed=21 + min_blocks)
+    res, h, out, b, blocks = _run(eng_cls, T, basis, 16, 4, min_blocks, max_iters=53)
+    res1, h1, out1, b1, _ = _run(eng_cls, T, basis, 16, 1, max_iters=53)
+    assert blocks == max(min_blocks, 5)
+    assert h == h1 and res.iters == res1.iters and out.tobytes() == out1.tobytes()
+    ref, rb = T.copy(), basis.copy()
+    st, hist = O.solve_tableau(ref, rb, max_iters=53)
+    assert [tuple(x) for x in h] == hist and np.array_equal(out, ref)
+
+
+def test_chain_xcd_falls_back_to_spread(eng_cls):
+    """Mode 4 where the one-XCD chain does not fit: K = 28 (its LDS histories
+    exceed 160 KiB) and a tableau wider than 32 x 512 columns run the spread
+    chain, same bytes."""
+    T, basis = _random_tableau(301, 20400, seed=6)
+    _, h, out, _, blocks = _run(eng_cls, T, basis, 24, 4, max_iters=30)
+    _, h1, out1, _, _ = _run(eng_cls, T, basis, 24, 1, max_iters=30)
+    assert blocks == 80 and h == h1 and out.tobytes() == out1.tobytes()
+    T, basis = _random_tableau(301, 2051, seed=7)
+    _, h, out, _, blocks = _run(eng_cls, T, basis, 28, 4, max_iters=60)
+    _, h1, out1, _, _ = _run(eng_cls, T, basis, 28, 1, max_iters=60)
+    assert blocks == 9 and h == h1 and out.tobytes() == out1.tobytes()
+
+
 @pytest.mark.parametrize("mode,nb", [(0, 80), (2, 80), (3, 40)])
 def test_chain_wide_tableau_more_than_64_blocks(eng_cls, mode, nb):
     """N > 64 x 256 columns: B = 80 blocks of 256 threads (two records per
@@ -107,7 +137,7 @@ def test_chain_wide_tableau_more_than_64_blocks(eng_cls, mode, nb):
 
 
 @pytest.mark.parametrize("K", [8, 24])
-@pytest.mark.parametrize("mode,nb", [(0, 64), (2, 64), (3, 32)])
+@pytest.mark.parametrize("mode,nb", [(0, 64), (2, 64), (3, 32), (4, 32)])
 def test_chain_config3_width_rhs_column_rides_along(eng_cls, K, mode, nb):
     """Config 3's width: N - 1 = 16384 candidate columns = 64 x 256, so the
     grid is 64 blocks (one record per polling lane) and the RHS column is kept
@@ -124,8 +154,8 @@ def test_chain_config3_width_rhs_column_rides_along(eng_cls, K, mode, nb):
     assert [tuple(x) for x in h] == hist and np.array_equal(out, ref)
 
 
-@pytest.mark.parametrize("K", [4, 32])
-@pytest.mark.parametrize("mode", [0, 3])
+@pytest.mark.parametrize("K", [4, 24, 32])
+@pytest.mark.parametrize("mode", [0, 3, 4])
 def test_chain_degenerate_bland_full_solve(eng_cls, K, mode):
     from simplex_amd import synth
     T, basis = synth.full_tableau("degenerate", 96, 96, seed=3)
@@ -259,7 +289,8 @@ def test_chain_budget_zero_runs_launch_per_phase(eng_cls):
         assert e.chain_stats()["persistent_calls"] == 1
 
 
-def test_chain_handshake_forced_abort_reruns_bit_exact(eng_cls):
+@pytest.mark.parametrize("mode", [0, 4])
+def test_chain_handshake_forced_abort_reruns_bit_exact(eng_cls, mode):
     """spx_set_chain_handshake(ctx, -1): every persistent window aborts at its
     start handshake (ST_NOTRES) before any block stores anything; spx_solve,
     spx_pivot and spx_pivot_at rerun the aborted window with the
@@ -267,7 +298,7 @@ def test_chain_handshake_forced_abort_reruns_bit_exact(eng_cls):
     spx_run_pivots cannot rerun: its abort surfaces at spx_state."""
     from simplex_amd.engine import SpxError
     T, basis = _random_tableau(300, 900, seed=71)
-    ref = _run(eng_cls, T, basis, 16, 0, max_iters=70)
+    ref = _run(eng_cls, T, basis, 16, mode, max_iters=70)
     Tc, bc = T.copy(), basis.copy()
     O.solve_tableau(Tc, bc, max_iters=71)  # the 70 pivots + one rule-chosen pivot
     nb = set(bc.tolist())
@@ -276,6 +307,7 @@ def test_chain_handshake_forced_abort_reruns_bit_exact(eng_cls):
     bc[5] = fc
     with eng_cls(0) as e:
         e.set_window(16)
+        e.set_chain(mode)
         e.load(T, basis)
         e.set_chain_handshake(-1)
         res = e.solve(max_iters=70)
@@ -372,25 +404,24 @@ def _shm_put(path, pid, blocks):
 def test_chain_admission_shared_across_processes(eng_cls):
     """The admission budget is shared by the processes on a GPU through
     /dev/shm/spx_chain_<bus id> (the reference runs gunicorn with 2 workers,
-    /root/reference/dockerfile:34).  With another live process holding all but
-    56 of the CUs' blocks, a 64-block chain is refused (launch-per-phase, same
+    /root/reference/dockerfile:34).  Budget 256: with another live process
+    holding 200 blocks, a 64-block chain is refused (launch-per-phase, same
     bytes); once that process is gone its entry is free and the chain is
     admitted; after spx_destroy (no explicit sync) this process's entry is 0."""
     import ctypes
     import subprocess
-    import torch
     from simplex_amd import _lib
     buf = ctypes.create_string_buffer(256)
     assert _lib.lib().spx_chain_shm_path(0, buf, 256) == 0
     path = buf.value.decode()
     assert path.startswith("/dev/shm/spx_chain_")
-    n_cu = torch.cuda.get_device_properties(0).multi_processor_count
     T, basis = _random_tableau(65, 16385, seed=64)  # config-3 width: 64 chain blocks
     ref = _run(eng_cls, T, basis, 24, 0, max_iters=48)
     assert ref[4] == 64
     other = subprocess.Popen(["sleep", "300"])
+    eng_cls.set_chain_budget(0, 256)
     try:
-        _shm_put(path, other.pid, n_cu - 56)
+        _shm_put(path, other.pid, 200)
         with eng_cls(0) as e:
             e.set_window(24)
             e.load(T, basis)
@@ -407,6 +438,7 @@ def test_chain_admission_shared_across_processes(eng_cls):
             e.run_pivots(4 * 24)  # no sync: released behind the launches, or at destroy
         assert not any(p == os.getpid() and b > 0 for p, b in _shm_entries(path))
     finally:
+        eng_cls.set_chain_budget(0, -1)
         if other.poll() is None:
             other.kill()
             other.wait()

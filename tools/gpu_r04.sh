@@ -12,7 +12,11 @@ PYT="python -u -m pytest -x -v --timeout 300 --timeout-method thread"
 for s in ${STEPS:-probe tests bench}; do
   case $s in
     probe) TAILN=12 run 120 xcd_probe.log ./tools/xcd_exchange_probe 2000 ;;
-    tests) run 900 pytest_sel.log $PYT ${TESTS:-tests/test_gpu_chain.py tests/test_gpu_peer_chain.py} ;;
+    tests) if [ -n "${KEXPR:-}" ]; then
+             run 900 pytest_sel.log $PYT ${TESTS:-tests/test_gpu_chain.py tests/test_gpu_peer_chain.py} -k "$KEXPR"
+           else
+             run 900 pytest_sel.log $PYT ${TESTS:-tests/test_gpu_chain.py tests/test_gpu_peer_chain.py}
+           fi ;;
     suite) run 1100 pytest_gpu.log $PYT -m gpu tests ;;
     bench) TAILN=1 run 300 bench_driver.log python bench.py --steps 20 --warmup 5 --cpu-seconds 0 ;;
     bench40) TAILN=1 run 300 bench40.log python bench.py --steps 40 --warmup 5 --cpu-seconds 0 ;;
@@ -21,6 +25,18 @@ for s in ${STEPS:-probe tests bench}; do
     phases) TAILN=30 run 200 phases24.log python tools/probe_phases.py --window 24 ;;
     smoke) run 200 smoke.log python -c "import __graft_entry__ as g; g.smoke()" ;;
     rocprof) run 400 rocprof.log rocprofv3 --kernel-trace --stats -d $O/prof -o bench --output-format csv -- python3 bench.py --steps 20 --warmup 5 --cpu-seconds 0 ;;
+    ab) for r in ${ROUNDS:-1 2 3}; do for c in ${CHAINS:-0 4}; do
+          TAILN=0 run 300 ab_c${c}_r$r.log python bench.py --chain $c --steps 40 --warmup 5 --cpu-seconds 0 ${ABARGS:-}
+          python - "$O/ab_c${c}_r$r.log" "$c" "$r" >> $O/ab.jsonl <<'PY'
+import json, sys
+l = [x for x in open(sys.argv[1]) if x.startswith("{")][-1]
+d = json.loads(l)
+print(json.dumps({"chain": int(sys.argv[2]), "round": int(sys.argv[3]), "value": round(d["value"], 1),
+                  "ms_per_step": round(d["ms_per_step"], 4), "flush_us": round(d["roofline"]["avg_launch_us"], 1),
+                  "frac": round(d["roofline"]["frac"], 4), "chain_blocks": d["config"]["chain_blocks"],
+                  "chain_us_per_pivot": round(d["chain"]["us_per_pivot"], 3)}))
+PY
+        done; done; cat $O/ab.jsonl ;;
     *) echo "unknown step $s"; exit 3 ;;
   esac
 done
