@@ -146,6 +146,7 @@ def cpu_baseline(m, n, seed, rule, budget_s, gpu_hist):
         k2 += 1
     el2 = time.perf_counter() - t0
     ok2 = matches(hist2)
+    host = _host_cpus()
     return {"value": k / el, "unit": "pivots/s", "cores": threads, "kind": "port",
             "sample": f"C/OpenMP oracle (oracle/spx_oracle.c), first {k} {rule} pivots of the "
                       f"same {m}x{n} tableau from the slack basis, {el:.1f} s, {threads} threads "
@@ -155,7 +156,40 @@ def cpu_baseline(m, n, seed, rule, budget_s, gpu_hist):
                           "seconds": el1},
             "numpy_1thread": {"value": k2 / el2, "pivots": k2, "seconds": el2,
                               "matches_gpu": bool(ok2)},
-            "host": _host_cpus()}
+            "all_cores": _all_cores_projection(k / el, threads, host, alg_bytes_per_pivot(m, n)),
+            "host": host}
+
+
+# Host DRAM peak by CPU model (spec): EPYC 9005 "Turin" sockets have 12 DDR5-6400
+# channels = 614.4 GB/s each.
+HOST_DRAM_PEAK = {"EPYC 9575F": 614.4}
+
+
+def alg_bytes_per_pivot(m, n):
+    """Bytes one pivot must move on config 3 from the slack basis: read and
+    write every element of the n + 1 touched columns."""
+    return 16.0 * m * (n + 1)
+
+
+def _all_cores_projection(v, threads, host, bytes_per_pivot):
+    """The C oracle on every physical core is NOT run: the harness gives this
+    job 16 threads (OMP_NUM_THREADS=16 on the box, the other cores belong to
+    other jobs).  What is reported instead is an upper bound: the measured
+    rate scaled linearly to all physical cores, capped by the host's DRAM
+    roofline (sockets x spec bandwidth / bytes per pivot) -- the CPU path is
+    as memory-bound as the GPU's."""
+    phys = host.get("physical_cores")
+    model = host.get("model") or ""
+    per_socket = next((bw for k, bw in HOST_DRAM_PEAK.items() if k in model), None)
+    peak = per_socket * host["sockets"] if (per_socket and host.get("sockets")) else None
+    lin = v * phys / threads if phys and threads else None
+    roof = peak * 1e9 / bytes_per_pivot if peak else None
+    cands = [x for x in (lin, roof) if x]
+    return {"measured": False,
+            "why": "the harness caps this job at 16 host threads (OMP_NUM_THREADS=16)",
+            "physical_cores": phys, "linear_projection": lin,
+            "host_dram_peak_GBps": peak, "dram_roofline_pivots_per_s": roof,
+            "upper_bound": min(cands) if cands else None}
 
 
 def _host_cpus():

@@ -1188,7 +1188,9 @@ __global__ __launch_bounds__(CB) void chain_xcd_kernel(
       gu32* xc = (gu32*)win.xcnt;
       const unsigned tk =
           __hip_atomic_fetch_add(xc + xcc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (tk == (unsigned)B - 1u) {  // the B-th arrival on my XCD: claim the chain
+      // the B-th arrival on my XCD claims the chain (a negative bound: the
+      // forced-ABORT test hook, no claim)
+      if (tk == (unsigned)B - 1u && hs_bound >= 0) {
         unsigned z = 0u;
         __hip_atomic_compare_exchange_strong(xc + 8, &z, xcc + 1u, __ATOMIC_RELAXED,
                                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
