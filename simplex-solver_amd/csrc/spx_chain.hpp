@@ -49,14 +49,18 @@ namespace spx {
 // events 0 ratio record stored, 1 ratio poll done, 2 entering record stored,
 // 3 entering poll done (of slot q+1's ratio phase)
 __device__ unsigned long long spx_probe_chain[32 * 4 * 256];
-#define SPX_PROBE_CHAIN(q, ev)                                                            \
+#define SPX_PROBE_CHAIN_R(role, q, ev)                                                    \
   do {                                                                                   \
-    if (threadIdx.x == 0 && blockIdx.x < 256 && (q) < 32)                                \
-      spx_probe_chain[((q) * 4 + (ev)) * 256 + blockIdx.x] = __builtin_amdgcn_s_memrealtime(); \
+    if (threadIdx.x == 0 && (role) < 256 && (q) < 32)                                    \
+      spx_probe_chain[((q) * 4 + (ev)) * 256 + (role)] = __builtin_amdgcn_s_memrealtime(); \
   } while (0)
+#define SPX_PROBE_CHAIN(q, ev) SPX_PROBE_CHAIN_R(blockIdx.x, q, ev)
 #else
 #define SPX_PROBE_CHAIN(q, ev) \
   do {                         \
+  } while (0)
+#define SPX_PROBE_CHAIN_R(role, q, ev) \
+  do {                                 \
   } while (0)
 #endif
 
@@ -1271,7 +1275,7 @@ __global__ __launch_bounds__(CB) void chain_xcd_kernel(
   int32_t stop_status = ST_RUNNING;
   for (; q < npiv; ++q) {
     // ================= ratio phase q =================
-    SPX_PROBE(q, 0, 0, true);
+    SPX_PROBE_ROLE(b, q, 0, 0, true);
     int64_t c;
     double zc;
     int wb = 0;
@@ -1293,7 +1297,7 @@ __global__ __launch_bounds__(CB) void chain_xcd_kernel(
           bc_val = e.a;
           bc_blk = (int)e.b;
         }
-        SPX_PROBE_CHAIN(q - 1, 3);
+        SPX_PROBE_CHAIN_R(b, q - 1, 3);
       }
       __syncthreads();
       c = bc_idx;
@@ -1301,7 +1305,7 @@ __global__ __launch_bounds__(CB) void chain_xcd_kernel(
       wb = bc_blk;
       if (c == -2) return;  // a wait timed out (ST_FAULT stored)
     }
-    SPX_PROBE(q, 0, 1, true);
+    SPX_PROBE_ROLE(b, q, 0, 1, true);
     if (forced_c >= 0) {
       c = forced_c;
       zc = obj[c];  // (forced pivots are single-pivot windows: q == 0)
@@ -1322,7 +1326,7 @@ __global__ __launch_bounds__(CB) void chain_xcd_kernel(
         !load_extras<0>(gr_enter, wb, ENTER_HDR, q, 0, rec_tag(W, q - 1, GK_ENTER), pcl, unused,
                         st))
       return;
-    SPX_PROBE(q, 2, 0, fv != 12345.678 && pcl != 12345.678);  // loads arrived
+    SPX_PROBE_ROLE(b, q, 2, 0, fv != 12345.678 && pcl != 12345.678);  // loads arrived
     // RHS: apply slot q-1 (the slots before it are already in bcur)
     if (q > 0) bcur = apply_sel(bcur, i == r_prev, false, true, f_prev, prhs, skip);
     // apply_sel's special cases as masks: column c entered earlier in this
@@ -1373,7 +1377,7 @@ __global__ __launch_bounds__(CB) void chain_xcd_kernel(
         }
       }
     }
-    SPX_PROBE(q, 2, 1, fv != 12345.678);  // slots applied
+    SPX_PROBE_ROLE(b, q, 2, 1, fv != 12345.678);  // slots applied
     if constexpr (LH) {
       if (trok) fsl[q][trc] = fv;
     } else {
@@ -1390,7 +1394,7 @@ __global__ __launch_bounds__(CB) void chain_xcd_kernel(
         if (rq == rq) kmin2(k, rq, rule == RULE_BLAND ? bas : i, i, 0.0, 0.0);
       }
     }
-    SPX_PROBE(q, 0, 2, fv != 12345.678);
+    SPX_PROBE_ROLE(b, q, 0, 2, fv != 12345.678);
     // publish: the wave winner puts its f history and RHS in LDS, the block's
     // winner is published by wave 0 (rows grow with the lane: Dantzig's tie key)
     k = key_of_lane(k, wave_argmin(k.v, k.t, k.row >= 0, rule != RULE_BLAND));
@@ -1405,9 +1409,9 @@ __global__ __launch_bounds__(CB) void chain_xcd_kernel(
       }
     }
     if (lane == 0) sk[w] = KeyP{k.v, k.t, k.row, 0.0, (double)w};
-    SPX_PROBE(q, 2, 2, k.v != 12345.678);  // wave argmin + LDS hand-off issued
+    SPX_PROBE_ROLE(b, q, 2, 2, k.v != 12345.678);  // wave argmin + LDS hand-off issued
     __syncthreads();
-    SPX_PROBE(q, 2, 3, true);              // every wave of the block arrived
+    SPX_PROBE_ROLE(b, q, 2, 3, true);              // every wave of the block arrived
     if (w0) {
       publish_local<NW, true, true>(gr_ratio, b, rec_tag(W, q, GK_RATIO), q + 1, sk,
                                [&](int ww, int64_t row, int x) -> double {
@@ -1417,14 +1421,14 @@ __global__ __launch_bounds__(CB) void chain_xcd_kernel(
                                  else
                                    return hl[ww][x];
                                });
-      SPX_PROBE_CHAIN(q, 0);
+      SPX_PROBE_CHAIN_R(b, q, 0);
     }
     // f_q for the flush / row_fix (later kernels): stored after the record, so
     // these stores never queue in front of it
     if (ilive) win.F[(int64_t)q * ld + i] = fv;
-    SPX_PROBE(q, 0, 3, true);
+    SPX_PROBE_ROLE(b, q, 0, 3, true);
     // ================= norm phase q =================
-    SPX_PROBE(q, 1, 0, true);
+    SPX_PROBE_ROLE(b, q, 1, 0, true);
     if (w0) {
       KeyP rk;
       const unsigned rtag = rec_tag(W, q, GK_RATIO);
@@ -1435,13 +1439,13 @@ __global__ __launch_bounds__(CB) void chain_xcd_kernel(
         bc_idx = ok ? rk.row : -2;
         bc_blk = (int)rk.b;
       }
-      SPX_PROBE_CHAIN(q, 1);
+      SPX_PROBE_CHAIN_R(b, q, 1);
     }
     __syncthreads();
     const int64_t r = bc_idx;
     wb = bc_blk;
     if (r == -2) return;
-    SPX_PROBE(q, 1, 1, true);
+    SPX_PROBE_ROLE(b, q, 1, 1, true);
     if (q == 0 && leader) *win.epoch = W;  // every block has read E (its record carries W)
     if (r < 0) {
       stop_status = ST_UNBOUNDED;
@@ -1458,7 +1462,7 @@ __global__ __launch_bounds__(CB) void chain_xcd_kernel(
     if (!load_extras<1>(gr_ratio, wb, RATIO_HDR + 2, q + 1, RATIO_HDR, rec_tag(W, q, GK_RATIO),
                         frl, ex, st))
       return;
-    SPX_PROBE(q, 3, 0, v != 12345.678 && frl != 12345.678);  // loads arrived
+    SPX_PROBE_ROLE(b, q, 3, 0, v != 12345.678 && frl != 12345.678);  // loads arrived
     const double piv = rdlane(frl, q);
     prhs = ex[0] / piv;  // p_q[rhs]: lazy_norm's p = v / piv of the RHS column
     // Special cases as masks: row r left earlier in the window (uniform: the
@@ -1509,7 +1513,7 @@ __global__ __launch_bounds__(CB) void chain_xcd_kernel(
         }
       }
     }
-    SPX_PROBE(q, 3, 1, v != 12345.678);  // slots applied
+    SPX_PROBE_ROLE(b, q, 3, 1, v != 12345.678);  // slots applied
     KeyP ek = keyp_none();
     double pq = 0.0;  // p_q[j]
     if (jlive) {
@@ -1557,7 +1561,7 @@ __global__ __launch_bounds__(CB) void chain_xcd_kernel(
       slot_c = c;
     }
     r_prev = r;
-    SPX_PROBE(q, 1, 2, v != 12345.678);
+    SPX_PROBE_ROLE(b, q, 1, 2, v != 12345.678);
     ek = key_of_lane(ek, wave_argmin(ek.v, ek.t, ek.row >= 0, true));  // columns grow with the lane
     if constexpr (LH) {
       psl[q][t] = pq;
@@ -1567,9 +1571,9 @@ __global__ __launch_bounds__(CB) void chain_xcd_kernel(
         if (s <= q) hl[w][s] = ps[s];
     }
     if (lane == 0) sk[w] = KeyP{ek.v, ek.t, ek.row, ek.a, (double)w};
-    SPX_PROBE(q, 3, 2, ek.v != 12345.678);  // wave argmin + LDS hand-off issued
+    SPX_PROBE_ROLE(b, q, 3, 2, ek.v != 12345.678);  // wave argmin + LDS hand-off issued
     __syncthreads();
-    SPX_PROBE(q, 3, 3, true);               // every wave of the block arrived
+    SPX_PROBE_ROLE(b, q, 3, 3, true);               // every wave of the block arrived
     if (w0) {
       if (q + 1 < npiv) {
         publish_local<NW, false, true>(gr_enter, b, rec_tag(W, q, GK_ENTER), q + 1, sk,
@@ -1590,7 +1594,7 @@ __global__ __launch_bounds__(CB) void chain_xcd_kernel(
         // keep an earlier kernel's keys
         for (int x = b + B; x < n_ep; x += B) store_key(enter_part + x, keyr_none());
       }
-      SPX_PROBE_CHAIN(q, 2);
+      SPX_PROBE_CHAIN_R(b, q, 2);
     }
     // stores for later kernels, after the record (never queued in front of it):
     // the pivot's bookkeeping (the flush and row_fix read p from the records)
@@ -1609,7 +1613,7 @@ __global__ __launch_bounds__(CB) void chain_xcd_kernel(
       }
     }
 
-    SPX_PROBE(q, 1, 3, true);
+    SPX_PROBE_ROLE(b, q, 1, 3, true);
   }
   // ---- the window ends after slot q (q pivots made) ----
   if (stop_status != ST_RUNNING && leader) {

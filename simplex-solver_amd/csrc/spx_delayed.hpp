@@ -49,6 +49,14 @@ __device__ unsigned long long spx_probe_buf[1024 + 2 * 8192];
       spx_probe_buf[(((slot) * 4 + (kind)) * 4 + (phase)) & 1023] =                          \
           __builtin_amdgcn_s_memrealtime();                                                  \
   } while (0)
+// the same, stamped by the block with role `role` (the one-XCD chain's block 0
+// may not take part)
+#define SPX_PROBE_ROLE(role, slot, kind, phase, cond)                                       \
+  do {                                                                                       \
+    if ((role) == 0 && threadIdx.x == 0 && (cond))                                           \
+      spx_probe_buf[(((slot) * 4 + (kind)) * 4 + (phase)) & 1023] =                          \
+          __builtin_amdgcn_s_memrealtime();                                                  \
+  } while (0)
 // flush waves: [2*(4*b + w)] = exit time, [.. + 1] = HW_ID | XCC_ID << 32 | columns << 40
 __device__ unsigned long long spx_probe_wave[2 * 4 * 8192];
 #define SPX_PROBE_WAVE(w, cols)                                                              \
@@ -66,6 +74,9 @@ __device__ unsigned long long spx_probe_wave[2 * 4 * 8192];
 #else
 #define SPX_PROBE(slot, kind, phase, cond) \
   do {                                     \
+  } while (0)
+#define SPX_PROBE_ROLE(role, slot, kind, phase, cond) \
+  do {                                                \
   } while (0)
 #define SPX_PROBE_BLOCK(which) \
   do {                         \
