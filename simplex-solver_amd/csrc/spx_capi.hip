@@ -262,6 +262,8 @@ int free_buffers(spx_ctx* ctx) {
   dfree(ctx->win.nlist);
   dfree(ctx->win.rec);
   dfree(ctx->win.xcnt);
+  dfree(ctx->win.colrow);
+  dfree(ctx->win.inexact);
   dfree(ctx->gr_enter);
   dfree(ctx->gr_ratio);
   ctx->loaded = false;
@@ -814,7 +816,9 @@ int enqueue_window_t(spx_ctx* ctx, int npiv, bool time_flush) {
   // a tail inside the flush measured 226 vs 182 us
   // (profiles/r03/ab_flush_tail_vs_rowfix.jsonl)
   hipLaunchKernelGGL(row_fix_kernel<KMAX>, dim3(ctx->nbn), dim3(BLK), 0, ctx->stream, ctx->A,
-                       ctx->ld, ctx->m_local, ctx->row0, ctx->N, ctx->win, npiv);
+                       ctx->ld, ctx->m_local, ctx->row0, ctx->N, ctx->win, npiv,
+                       (const State*)ctx->st, (const int64_t*)ctx->basis,
+                       ctx->sharded ? (int64_t)0 : ctx->m_local);
   HIPC(hipGetLastError());
   return SPX_OK;
 }
@@ -1073,6 +1077,10 @@ int alloc_common(spx_ctx* ctx, int64_t m_local, int64_t N, int64_t m_global, int
     HIPC(hipMalloc(&ctx->win.rec, sizeof(double) * RECW * N));
     HIPC(hipMalloc(&ctx->win.xcnt, sizeof(uint32_t) * 9));
     HIPC(hipMemsetAsync(ctx->win.xcnt, 0, sizeof(uint32_t) * 9, ctx->stream));
+    HIPC(hipMalloc(&ctx->win.colrow, sizeof(uint64_t) * N));
+    HIPC(hipMemsetAsync(ctx->win.colrow, 0, sizeof(uint64_t) * N, ctx->stream));
+    HIPC(hipMalloc(&ctx->win.inexact, N));
+    HIPC(hipMemsetAsync(ctx->win.inexact, 0, N, ctx->stream));
     HIPC(hipMemsetAsync(ctx->win.nlist, 0, sizeof(int32_t), ctx->stream));
     HIPC(hipMemsetAsync(ctx->win.rec, 0, sizeof(double) * RECW * N, ctx->stream));
     HIPC(hipMemsetAsync(ctx->win.F, 0, sizeof(double) * KW * ctx->ld, ctx->stream));
@@ -1544,6 +1552,16 @@ int spx_load_rows(spx_ctx* ctx, const double* A, int64_t m_local, int64_t cols, 
   if (m_global > 0)
     HIPC(hipMemcpyAsync(ctx->basis, basis, sizeof(int64_t) * m_global, hipMemcpyHostToDevice,
                         ctx->stream));
+  if (!ctx->sharded && m_local > 0) {
+    // the basic columns' exactness, for the chain's row gather (colrow_of)
+    hipLaunchKernelGGL(basis_exact_kernel, dim3((unsigned)m_local), dim3(BLK), 0, ctx->stream,
+                       (const double*)ctx->A, ctx->ld, m_local, cols,
+                       (const int64_t*)ctx->basis, ctx->win);
+    hipLaunchKernelGGL(basis_stamp_kernel, dim3((unsigned)((m_local + BLK - 1) / BLK)), dim3(BLK),
+                       0, ctx->stream, (const int64_t*)ctx->basis, m_local, cols, (int64_t)0,
+                       ctx->win);
+    HIPC(hipGetLastError());
+  }
   HIPC(hipStreamSynchronize(ctx->stream));
   ctx->loaded = true;
   return SPX_OK;

@@ -476,21 +476,37 @@ def test_chain_timing_events(eng_cls, mode):
 
 
 @pytest.mark.parametrize("K", [8, 24])
-def test_chain_basic_columns_not_unit_vectors_at_load(eng_cls, K):
+@pytest.mark.parametrize("mode", [0, 4])
+def test_chain_basic_columns_not_unit_vectors_at_load(eng_cls, K, mode):
     """Basic columns that are not exact unit vectors at load (a tiny entry, a
-    -0.0, 1 + ulp) are ordinary data: the chain must not assume their values."""
+    -0.0, 1 + ulp) are ordinary data: the chain must not assume their values
+    (the one-XCD chain synthesizes the row gather of basic columns that ARE
+    exact; these are flagged at load).  Forced pivots on the affected rows
+    make each of them the leaving row."""
     T, basis = _random_tableau(400, 1300, seed=40 + K)
-    m = T.shape[0] - 1
     T[3, basis[7]] = 1e-300          # basic column of row 7 with an extra entry
     T[11, basis[2]] = -0.0           # -0.0 is not +0.0
     T[5, basis[5]] = 1.0 + 2.0 ** -52  # not exactly 1
-    res, h, out, b, _ = _run(eng_cls, T, basis, K, 0, max_iters=3 * K + 3)
+    res, h, out, b, _ = _run(eng_cls, T, basis, K, mode, max_iters=3 * K + 3)
     res1, h1, out1, b1, _ = _run(eng_cls, T, basis, K, 1, max_iters=3 * K + 3)
     assert h == h1 and out.tobytes() == out1.tobytes() and np.array_equal(b, b1)
     ref, rb = T.copy(), basis.copy()
     st, hist = O.solve_tableau(ref, rb, max_iters=3 * K + 3)
     assert [tuple(x) for x in h] == hist and np.array_equal(out, ref)
-    del m
+    ref, rb = T.copy(), basis.copy()
+    with eng_cls(0) as e:
+        e.set_window(K)
+        e.set_chain(mode)
+        e.load(T, basis)
+        for r in (3, 11, 5):
+            nb = set(rb.tolist())
+            c = next(j for j in range(T.shape[1] - 1) if j not in nb and abs(ref[r, j]) > 0.05)
+            e.pivot_at(r, c)
+            O.pivot(ref, r, c)
+            rb[r] = c
+        e.solve(max_iters=2 * K + 1)
+        O.solve_tableau(ref, rb, max_iters=2 * K + 1)
+        assert np.array_equal(e.tableau(), ref) and np.array_equal(e.basis(), rb)
 
 
 def test_chain_after_single_pivots_on_the_same_context(eng_cls):

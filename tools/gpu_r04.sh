@@ -25,13 +25,16 @@ for s in ${STEPS:-probe tests bench}; do
     phases) TAILN=30 run 200 phases24.log python tools/probe_phases.py --window 24 ;;
     smoke) run 200 smoke.log python -c "import __graft_entry__ as g; g.smoke()" ;;
     rocprof) run 400 rocprof.log rocprofv3 --kernel-trace --stats -d $O/prof -o bench --output-format csv -- python3 bench.py --steps 20 --warmup 5 --cpu-seconds 0 ;;
-    ab) for r in ${ROUNDS:-1 2 3}; do for c in ${CHAINS:-0 4}; do
-          TAILN=0 run 300 ab_c${c}_r$r.log python bench.py --chain $c --steps 40 --warmup 5 --cpu-seconds 0 ${ABARGS:-}
-          python - "$O/ab_c${c}_r$r.log" "$c" "$r" >> $O/ab.jsonl <<'PY'
+    ab) # VARIANTS: label=lib:chain ... (lib relative to simplex-solver_amd/simplex_amd/lib)
+        for r in ${ROUNDS:-1 2 3}; do for v in ${VARIANTS:-spread=libspx.so:0 xcd=libspx.so:4}; do
+          lab=${v%%=*}; rest=${v#*=}; lib=${rest%%:*}; c=${rest#*:}
+          SPX_LIB=$PWD/simplex-solver_amd/simplex_amd/lib/$lib SPX_LIB_PARTIAL=1 TAILN=0 \
+            run 300 ab_${lab}_r$r.log python bench.py --chain $c --steps 40 --warmup 5 --cpu-seconds 0 ${ABARGS:-}
+          python - "$O/ab_${lab}_r$r.log" "$lab" "$r" >> $O/ab.jsonl <<'PY'
 import json, sys
 l = [x for x in open(sys.argv[1]) if x.startswith("{")][-1]
 d = json.loads(l)
-print(json.dumps({"chain": int(sys.argv[2]), "round": int(sys.argv[3]), "value": round(d["value"], 1),
+print(json.dumps({"variant": sys.argv[2], "round": int(sys.argv[3]), "value": round(d["value"], 1),
                   "ms_per_step": round(d["ms_per_step"], 4), "flush_us": round(d["roofline"]["avg_launch_us"], 1),
                   "frac": round(d["roofline"]["frac"], 4), "chain_blocks": d["config"]["chain_blocks"],
                   "chain_us_per_pivot": round(d["chain"]["us_per_pivot"], 3)}))
