@@ -818,7 +818,10 @@ int enqueue_window_t(spx_ctx* ctx, int npiv, bool time_flush) {
   hipLaunchKernelGGL(row_fix_kernel<KMAX>, dim3(ctx->nbn), dim3(BLK), 0, ctx->stream, ctx->A,
                        ctx->ld, ctx->m_local, ctx->row0, ctx->N, ctx->win, npiv,
                        (const State*)ctx->st, (const int64_t*)ctx->basis,
-                       ctx->sharded ? (int64_t)0 : ctx->m_local);
+                       // (the basic-column stamps only feed the one-XCD chain's row
+                       // gather: the spread chain measured slower with them,
+                       // profiles/r04/ab_basic_column_skip.jsonl)
+                       (xcd || ctx->chain_mode == 4) ? ctx->m_local : (int64_t)0);
   HIPC(hipGetLastError());
   return SPX_OK;
 }

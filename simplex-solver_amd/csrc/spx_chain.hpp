@@ -655,8 +655,6 @@ __global__ __launch_bounds__(CB) void chain_kernel(
   const int64_t ic = ilive ? i : 0;
   double o = obj[jc];
   uint32_t tg = jlive ? win.tag[jc] : 0u;
-  // my column's row if it is basic at the window start (-1: load the row)
-  const int64_t crow = jlive ? colrow_of(win, jc, it0) : -1;
   const uint32_t tg0 = tg;
   // The RHS column N-1 is never an entering candidate and its pivot-row value
   // is the ratio record's p_q[rhs] (the row owner's current RHS / pivot), so
@@ -895,8 +893,7 @@ __global__ __launch_bounds__(CB) void chain_kernel(
     }
     // row r on my column: stale + pending slots.  f_s[r] (lane s <= q, lane q
     // the pivot element) and the row's RHS from the winning ratio record
-    // (a column basic at the window start is exactly e_crow there: no load)
-    double v = crow >= 0 ? (crow == r ? 1.0 : 0.0) : A[jc * ld + r];
+    double v = A[jc * ld + r];
     if constexpr (LH) {  // my column's p history, read while the gathers are in flight
 #pragma unroll
       for (int s = 0; s < KMAX; ++s) ps[s] = psl[s][t];

@@ -16,6 +16,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
+#include <algorithm>
 #include <cstdlib>
 
 typedef __attribute__((address_space(1))) unsigned long long gu64;
@@ -101,7 +102,11 @@ __global__ __launch_bounds__(CB) void row_probe(unsigned long long* rec_, unsign
     const int64_t jw = (int64_t)me * cpb + t;
     bool hit = false;
     if (t < cpb && jw < ncw) {
-      const double* p = A + jw * ld * per + r * per;
+      // ld < 0: the 512-row panel layout, row r in panel r / 512 of 16 (each
+      // panel 512 rows x all columns, a column's piece 4 KiB): span 1.1 GB in
+      // all, 67 MB per gather
+      const double* p = ld >= 0 ? A + jw * ld * per + r * per
+                                : A + (r >> 9) * (512 * ncw * per) + jw * 512 * per + (r & 511) * per;
       if (width == 8) {
         hit = p[0] == 12345.678;
       } else if (width == 16) {
@@ -132,22 +137,49 @@ int main(int argc, char** argv) {
   CK(hipMalloc((void**)&tmo, sizeof(unsigned)));
   CK(hipMalloc((void**)&out, MAXB * sizeof(unsigned)));
   const int64_t LDF = 8448;  // config 3's padded column stride (doubles)
-  double* A;
-  const size_t abytes = (size_t)LDF * NC * sizeof(double) + 4096;
-  CK(hipMalloc((void**)&A, abytes));
-  CK(hipMemset(A, 0, abytes));
+  // every span's largest address: (wide column ncw-1) * ld * per + (M-1) * per
+  // < (NC + 8) * LDF + 2 * M doubles
+  const size_t abytes = ((size_t)LDF * (NC + 8) + 2 * (size_t)M + 4096) * sizeof(double);
+  double* Ad;  // default hipMalloc
+  CK(hipMalloc((void**)&Ad, abytes));
+  CK(hipMemset(Ad, 0, abytes));
+  double* Ac = nullptr;  // physically contiguous (hipDeviceMallocContiguous): bigger TLB fragments?
+  if (hipExtMallocWithFlags((void**)&Ac, abytes, hipDeviceMallocContiguous) != hipSuccess) {
+    (void)hipGetLastError();
+    Ac = nullptr;
+    printf("hipDeviceMallocContiguous: allocation refused\n");
+  } else {
+    CK(hipMemset(Ac, 0, abytes));
+  }
+  {
+    const int64_t ncw1 = NC, ncw2 = (NC + 1) / 2;
+    const int64_t mx1 = (15 * 512 * ncw1 + (ncw1 - 1) * 512 + 511) + 1;
+    const int64_t mx2 = (15 * 512 * ncw2 + (ncw2 - 1) * 512 + 511) * 2 + 2;
+    if ((size_t)std::max(mx1, mx2) * sizeof(double) > abytes) {
+      printf("panels16 exceeds the buffer\n");
+      return 2;
+    }
+  }
   hipStream_t s;
   CK(hipStreamCreate(&s));
   hipEvent_t a, b;
   CK(hipEventCreate(&a));
   CK(hipEventCreate(&b));
+  // spans: "1.1GB" the config-3 column stride; "panel" a 512-row panel layout
+  // (4 KiB per column: one row gather touches 67 MB); "compact" ~1 MB
+  struct Sp { const char* name; int64_t ld8; bool contig; } spans[] = {
+      {"1.1GB", LDF, false}, {"1.1GB-contig", LDF, true}, {"panel", 512, false},
+      {"panels16", -1, false}, {"compact", 8, false}};
   for (int xcd = 0; xcd < 2; ++xcd)
-    for (int width : {8, 16, 32})
-      for (int64_t ld : {LDF, (int64_t)8})  // full span, or compact (ld * per * 8 B per column)
-      {
-        // compact: consecutive wide columns 64 B apart -> one row gather touches ~1 MB
-        const int64_t ldd = ld == LDF ? LDF : 8 / (width / 8) > 0 ? 8 / (width / 8) : 1;
-        const int P = xcd ? 32 : 64, CB = xcd ? 512 : 256;
+    for (int width : {8, 16})
+      for (const Sp& sp : spans) {
+        if (sp.contig && !Ac) continue;
+        const double* A = sp.contig ? Ac : Ad;
+        const int per = width / 8;
+        const int64_t ldd = sp.ld8 == 8 ? (8 / per > 0 ? 8 / per : 1) : sp.ld8;
+        // panels16 bound: (15 * 512 * ncw + (ncw - 1) * 512 + 511) * per + per - 1 doubles
+        // < 16 * 512 * 16393 * 2 < abytes / 8 (checked on the host below)
+        const int P = xcd ? 32 : 64;
         float best = 1e30f;
         bool fail = false;
         for (int rep = 0; rep < 3 && !fail; ++rep) {
@@ -170,15 +202,14 @@ int main(int argc, char** argv) {
           CK(hipMemcpy(&tm, tmo, sizeof(unsigned), hipMemcpyDeviceToHost));
           if (tm) {
             printf("%s width=%d span=%s: TIMEOUT\n", xcd ? "xcd32x512" : "spread64x256", width,
-                   ld == LDF ? "1.1GB" : "compact");
+                   sp.name);
             fail = true;
           }
           best = ms < best ? ms : best;
         }
         if (!fail)
-          printf("%-13s width=%2d B span=%-7s  %.3f us per {exchange + row gather}\n",
-                 xcd ? "xcd32x512" : "spread64x256", width, ld == LDF ? "1.1GB" : "compact",
-                 1e3 * best / iters);
+          printf("%-13s width=%2d B span=%-12s  %.3f us per {exchange + row gather}\n",
+                 xcd ? "xcd32x512" : "spread64x256", width, sp.name, 1e3 * best / iters);
         fflush(stdout);
       }
   return 0;
