@@ -447,7 +447,7 @@ def test_chain_admission_shared_across_processes(eng_cls):
 def test_chain_set_validated(eng_cls):
     with eng_cls(0) as e:
         with pytest.raises(Exception):
-            e.set_chain(4)
+            e.set_chain(5)
         with pytest.raises(Exception):
             e.set_chain(0, 300)
 
