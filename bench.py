@@ -67,7 +67,8 @@ def parse():
     ap.add_argument("--chain", type=int, default=0,
                     help="window pivot chain: 0 one persistent launch per window (default, "
                          "single GPU), 1 two launches per pivot, 2 / 3 persistent with 256- / "
-                         "512-thread blocks")
+                         "512-thread blocks, 4 / 5 persistent on one XCD (512-thread / "
+                         "two 256-thread blocks per CU)")
     ap.add_argument("--chain-blocks", type=int, default=0, help="persistent chain grid (0: minimum)")
     ap.add_argument("--peer", type=int, default=1,
                     help="N > 1 windows: 1 the row-sharded persistent chain (peer records over "
@@ -85,7 +86,7 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=15.0,
                     help="budget of the CPU-baseline sample (0 disables)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles",
-                                                           "traffic_r03.json"))
+                                                           "traffic_r04.json"))
     return ap.parse_args()
 
 

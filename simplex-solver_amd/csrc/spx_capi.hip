@@ -468,14 +468,17 @@ int64_t chain_need(int64_t N, int64_t rows, int cb, int min_blocks) {
 // refused admission, or a tableau wider than CB x CUs columns).  Row shards
 // take the geometry every rank agreed on at spx_peer_import /
 // spx_peer_chain_local (shard_geometry), so no rank decides alone.
-// The one-XCD chain (chain_xcd_kernel, mode 4): B blocks of 512 threads on one
-// XCD, each owning <= 512 columns and <= 256 rows, the window histories in LDS
-// (K <= 24).  Returns B, or 0 when the tableau or the window does not fit.
-int chain_xcd_blocks(const spx_ctx* ctx) {
+// The one-XCD chain (chain_xcd_kernel): mode 4, B blocks of 512 threads on one
+// XCD (one per CU), each owning <= 512 columns and <= 256 rows; mode 5, B
+// blocks of 256 threads (two per CU), <= 256 columns and <= 128 rows.  The
+// window histories live in LDS (K <= 24).  Returns B, or 0 when the tableau or
+// the window does not fit one XCD.
+int chain_xcd_blocks(const spx_ctx* ctx, int cb) {
   if (ctx->sharded || ctx->win_k > 24) return 0;
-  const int per_xcd = std::max(1, ctx->n_cu / 8);
-  const int64_t need = std::max<int64_t>({(ctx->N - 1 + 511) / 512, (ctx->m_local + 255) / 256,
-                                          1, (int64_t)ctx->chain_min_blocks});
+  const int per_xcd = std::max(1, ctx->n_cu / 8) * (cb == 256 ? 2 : 1);
+  const int64_t need = std::max<int64_t>({(ctx->N - 1 + cb - 1) / cb,
+                                          (ctx->m_local + cb / 2 - 1) / (cb / 2), 1,
+                                          (int64_t)ctx->chain_min_blocks});
   return need <= per_xcd && need <= 64 ? (int)need : 0;
 }
 
@@ -497,10 +500,11 @@ int chain_blocks(spx_ctx* ctx, int* cb_out = nullptr, bool ignore_admission = fa
   }
   if (ctx->chain_denied && !ignore_admission) return 0;
   if (!ctx->n_cu) ctx->n_cu = device_cus(ctx->device);
-  if (ctx->chain_mode == 4) {  // the one-XCD chain where it fits, else the spread one
-    const int bx = chain_xcd_blocks(ctx);
+  if (ctx->chain_mode >= 4) {  // the one-XCD chain where it fits, else the spread one
+    const int xcb = ctx->chain_mode == 5 ? 256 : 512;
+    const int bx = chain_xcd_blocks(ctx, xcb);
     if (bx > 0) {
-      if (cb_out) *cb_out = 512;
+      if (cb_out) *cb_out = xcb;
       if (xcd_out) *xcd_out = true;
       return bx;
     }
@@ -725,11 +729,13 @@ int enqueue_window_t(spx_ctx* ctx, int npiv, bool time_flush) {
     if (rc) return rc;
   }
   if (B > 0 && xcd) {
-    // one 512-thread block per CU; the first XCD to gather B of them runs the chain
+    // one 512-thread block per CU (mode 5: two 256-thread blocks); the first
+    // XCD to gather B of them runs the chain
     const int cpb = (int)((ctx->N - 1 + B - 1) / B);
     const int rpb = (int)std::max<int64_t>(1, (ctx->m_local + B - 1) / B);
     if constexpr (KMAX <= 24) {
-      hipLaunchKernelGGL(chain_xcd_kernel<KMAX>, dim3(ctx->n_cu), dim3(512), 0, ctx->stream,
+      hipLaunchKernelGGL((cb == 256 ? chain_xcd_kernel<KMAX, 256> : chain_xcd_kernel<KMAX, 512>),
+                         dim3(cb == 256 ? 2 * ctx->n_cu : ctx->n_cu), dim3(cb), 0, ctx->stream,
                          ctx->enter_part, ctx->st, (const Params*)ctx->prm,
                          std::max(NWAVE * ctx->nbn, B), (const double*)ctx->A, ctx->ld,
                          ctx->m_local, ctx->N, ctx->obj, ctx->win, npiv, ctx->basis, ctx->hist,
@@ -821,7 +827,7 @@ int enqueue_window_t(spx_ctx* ctx, int npiv, bool time_flush) {
                        // (the basic-column stamps only feed the one-XCD chain's row
                        // gather: the spread chain measured slower with them,
                        // profiles/r04/ab_basic_column_skip.jsonl)
-                       (xcd || ctx->chain_mode == 4) ? ctx->m_local : (int64_t)0);
+                       (xcd || ctx->chain_mode >= 4) ? ctx->m_local : (int64_t)0);
   HIPC(hipGetLastError());
   return SPX_OK;
 }
@@ -2052,8 +2058,8 @@ int spx_get_elim_variant(const spx_ctx* ctx, int64_t out[7]) {
 // its minimum (tuning; 0 = minimum).
 int spx_set_chain(spx_ctx* ctx, int mode, int min_blocks) {
   if (!ctx) return SPX_E_ARG;
-  CHECK_ARG(mode >= 0 && mode <= 4 && min_blocks >= 0 && min_blocks <= CHAIN_MAX_BLOCKS,
-            "chain mode must be 0..4, min_blocks 0..256");
+  CHECK_ARG(mode >= 0 && mode <= 5 && min_blocks >= 0 && min_blocks <= CHAIN_MAX_BLOCKS,
+            "chain mode must be 0..5, min_blocks 0..256");
   ctx->chain_mode = mode;
   ctx->chain_min_blocks = min_blocks;
   drop_graphs(ctx);

@@ -1115,7 +1115,8 @@ __global__ __launch_bounds__(CB) void chain_kernel(
 // on one XCD").  The spread chain's blocks are dealt over all 8 XCDs, so both
 // exchanges of a pivot are cross-XCD round trips (write-through sc1 granules,
 // ~2.2 us each with 64 blocks).  Here the grid is one 512-thread block per CU
-// (its LDS keeps it alone there) and only B <= 32 blocks of ONE XCD run the
+// (its LDS keeps it alone there; mode 5: two 256-thread blocks per CU) and
+// only B <= 32 (64) blocks of ONE XCD run the
 // chain: every block reads HW_REG_XCC_ID and takes a ticket on its XCD's
 // counter; the first XCD to hand out B tickets is chosen by a compare-and-swap
 // (or, after st->hs_ticks without one, ABORT: the window reports ST_NOTRES and
@@ -1126,13 +1127,14 @@ __global__ __launch_bounds__(CB) void chain_kernel(
 // 2.18 spread, the two gathers of a pivot 0.65 us slower from 32 CUs.  The
 // participants are co-resident by construction (each took its ticket while
 // running).  Block role b owns columns [b*cpb, ...) (one per thread, cpb <=
-// 512) and rows [b*rpb, ...) (rpb <= 256, on waves 1..4); the window
-// histories live in LDS (psl: 512 columns, fsl: 256 rows; KMAX <= 24 fits the
-// 160 KiB).  The arithmetic is chain_kernel's, operation for operation, so the
+// CB) and rows [b*rpb, ...) (rpb <= CB/2, on the waves after wave 0); the
+// window histories live in LDS (psl: CB columns, fsl: CB/2 rows; KMAX <= 24
+// fits the 160 KiB once or twice).  The arithmetic is chain_kernel's, operation for operation, so the
 // results are the same bytes.  win.xcnt is zeroed by the window's row_fix.
 // ---------------------------------------------------------------------------
 template <int KMAX, int CB = 512>
-__global__ __launch_bounds__(CB) void chain_xcd_kernel(
+__global__ __launch_bounds__(CB) __attribute__((amdgpu_waves_per_eu(CB == 256 ? 2 : 1)))
+void chain_xcd_kernel(
     Key* __restrict__ enter_part, State* st, const Params* __restrict__ prm, int n_ep,
     const double* __restrict__ A, int64_t ld, int64_t m, int64_t N, double* __restrict__ obj,
     Window win, int npiv, int64_t* __restrict__ basis, int64_t* __restrict__ hist,
@@ -1143,8 +1145,13 @@ __global__ __launch_bounds__(CB) void chain_xcd_kernel(
   constexpr int CH = KMAX % 8 == 0 ? 8 : KMAX % 4 == 0 ? 4 : 2;
   // the window histories in LDS, slot-major: p_s[j] one column per thread,
   // f_s[i] one row per thread of waves 1..4 (RMAX rows per block)
-  constexpr int RMAX = 256;
-  static_assert(CB == 512 && KMAX * (CB + RMAX) * 8 <= 150 * 1024, "LDS: one block per CU");
+  // CB = 512: one block per CU (32 per XCD); CB = 256 (mode 5): two blocks
+  // per CU, 64 per XCD -- the spread chain's 4-wave blocks (its barrier and
+  // publish costs) with the one-XCD exchange
+  constexpr int RMAX = CB / 2;
+  static_assert((CB == 512 && KMAX * (CB + RMAX) * 8 <= 150 * 1024) ||
+                    (CB == 256 && KMAX * (CB + RMAX) * 8 <= 76 * 1024),
+                "LDS: one 512-thread or two 256-thread blocks per CU");
   constexpr bool LH = true;
   __shared__ double fsl[KMAX][RMAX];
   __shared__ double psl[KMAX][CB];

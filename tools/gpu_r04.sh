@@ -22,9 +22,11 @@ for s in ${STEPS:-probe tests bench}; do
     bench40) TAILN=1 run 300 bench40.log python bench.py --steps 40 --warmup 5 --cpu-seconds 0 ;;
     benchcpu) TAILN=1 run 400 bench_cpu.log python bench.py --cpu-seconds 15 ;;
     same) TAILN=1 run 400 bench_same.log python -m torch.distributed.run --nnodes=1 --nproc-per-node=2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --same-device --steps 20 --warmup 5 --cpu-seconds 0 ;;
-    phases) TAILN=30 run 200 phases24.log python tools/probe_phases.py --window 24 ;;
+    phases) TAILN=30 run 200 phases24${PHTAG:-}.log python tools/probe_phases.py --window 24 ${PHARGS:-} ;;
     smoke) run 200 smoke.log python -c "import __graft_entry__ as g; g.smoke()" ;;
     rocprof) run 400 rocprof.log rocprofv3 --kernel-trace --stats -d $O/prof -o bench --output-format csv -- python3 bench.py --steps 20 --warmup 5 --cpu-seconds 0 ;;
+    pmcf|pmcw) c=FETCH_SIZE; [ $s = pmcw ] && c=WRITE_SIZE
+        run 300 $s.log rocprofv3 --kernel-trace --pmc $c -d $O/$s -o p --output-format csv -- python3 bench.py --steps 20 --warmup 5 --cpu-seconds 0 ;;
     ab) # VARIANTS: label=lib:chain ... (lib relative to simplex-solver_amd/simplex_amd/lib)
         for r in ${ROUNDS:-1 2 3}; do for v in ${VARIANTS:-spread=libspx.so:0 xcd=libspx.so:4}; do
           lab=${v%%=*}; rest=${v#*=}; lib=${rest%%:*}; c=${rest#*:}
