@@ -380,8 +380,9 @@ def main():
         c_ms, c_n = eng.chain_timing(reset=True)
         eng.set_chain_timing(False)
         nb = eng.chain_blocks()
-        chain = {"kernel": "spx::chain_kernel" if nb else
-                 "spx::lazy_ratio_kernel + spx::lazy_norm_kernel",
+        chain = {"kernel": ("spx::chain_shard_kernel" if world > 1 else
+                            "spx::chain_xcd_kernel" if args.chain >= 4 else "spx::chain_kernel")
+                 if nb else "spx::lazy_ratio_kernel + spx::lazy_norm_kernel",
                  "bound": "latency: two in-launch all-to-all exchanges and two dependent "
                           "HBM gathers per pivot (DESIGN.md 4b)",
                  "blocks": nb, "avg_launch_us": 1e3 * c_ms / max(c_n, 1),

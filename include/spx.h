@@ -219,7 +219,7 @@ int spx_set_chain_timing(spx_ctx* ctx, int on);
 int spx_chain_timing(spx_ctx* ctx, double* total_ms, int64_t* count, int reset);
 /* Pivot chain of a window (the K pivot choices before its flush): mode 0
  * (default) runs them as ONE persistent launch when the tableau fits (at most
- * 512 x CUs columns and rows, single-GPU contexts; DESIGN.md §4c), mode 1 as two
+ * 512 x CUs columns and rows, single-GPU contexts; DESIGN.md §4b), mode 1 as two
  * launches per pivot, modes 2 / 3 force the persistent chain's 256- / 512-thread
  * blocks, modes 4 / 5 run the persistent chain on ONE XCD (one 512-thread /
  * two 256-thread blocks per CU; K <= 24 and a tableau that fits 32 CUs, else
