@@ -238,7 +238,8 @@ int spx_get_chain(spx_ctx* ctx, int* blocks);
  * launch-per-phase chain. */
 int spx_set_chain_budget(int device, int blocks);
 /* The budget is shared by every process using the same GPU through a table in
- * /dev/shm (entries {pid, blocks} under flock; dead processes' entries free;
+ * /dev/shm (entries {pid, blocks, start time} under flock; entries of dead
+ * processes, or of a pid since reused, are free;
  * SPX_CHAIN_SHM=0 turns it off).  This writes the table's path for `device`
  * (at most cap bytes with the terminating NUL). */
 int spx_chain_shm_path(int device, char* out, int cap);

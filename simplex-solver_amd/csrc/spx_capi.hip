@@ -528,7 +528,7 @@ int chain_blocks(spx_ctx* ctx, int* cb_out = nullptr, bool ignore_admission = fa
 //
 // Across processes (gunicorn's two workers, /root/reference/dockerfile:34)
 // the budget is shared through a table in /dev/shm/spx_chain_<PCI bus id>: 64
-// entries {pid, blocks}, read and written under flock.  Each process keeps
+// entries {pid, blocks, start time}, read and written under flock.  Each process keeps
 // its entry equal to its in-flight blocks on that GPU; a chain is admitted
 // only when every live process's blocks plus its own fit the budget.  Entries
 // of dead processes (kill(pid, 0) -> ESRCH) count as free, and a process
@@ -538,7 +538,35 @@ int chain_blocks(spx_ctx* ctx, int* cb_out = nullptr, bool ignore_admission = fa
 constexpr int SHM_SLOTS = 64;
 struct ShmEntry {
   int32_t pid, blocks;
+  uint64_t start;  // the process's start time (/proc/<pid>/stat): a reused pid is not it
 };
+static_assert(sizeof(ShmEntry) == 16, "the table's on-disk entry");
+
+// Start time of a live process in clock ticks since boot (0: unknown).
+uint64_t proc_start(int32_t pid) {
+  char path[64];
+  std::snprintf(path, sizeof(path), "/proc/%d/stat", (int)pid);
+  FILE* f = std::fopen(path, "r");
+  if (!f) return 0;
+  char buf[1024];
+  const size_t n = std::fread(buf, 1, sizeof(buf) - 1, f);
+  std::fclose(f);
+  buf[n] = 0;
+  const char* p = std::strrchr(buf, ')');  // the command name may hold spaces
+  if (!p) return 0;
+  // fields after the name: state (3) ... starttime (22)
+  int field = 2;
+  for (++p; *p && field < 22; ++p)
+    if (*p == ' ') ++field;
+  return field == 22 ? std::strtoull(p, nullptr, 10) : 0;
+}
+
+// Is the table entry's process alive (and the same process that wrote it)?
+bool shm_entry_live(const ShmEntry& e) {
+  if (!(kill(e.pid, 0) == 0 || errno == EPERM)) return false;
+  const uint64_t st = proc_start(e.pid);
+  return e.start == 0 || st == 0 || st == e.start;
+}
 
 struct ShmTable {
   int fd = -1;
@@ -589,10 +617,14 @@ int shm_fd_locked(ChainAdmission& a, int device) {
   return t.fd;
 }
 
-// Under the table's flock: the blocks of every OTHER live process, and (when
-// mine >= 0) this process's entry set to `mine`.  Returns -1 when the table
-// is unavailable (the process-local count then decides alone).
-int shm_exchange(int fd, int mine) {
+// Under the table's flock, in one critical section: the blocks of every OTHER
+// live process; then, if `admit` says those plus this process's own fit
+// (admit == nullptr: always), this process's entry set to `mine` (mine < 0:
+// read only).  Returns the others' blocks, or -1 when the table is
+// unavailable (the process-local count then decides alone); *ok the verdict.
+template <typename Admit>
+int shm_exchange(int fd, int mine, Admit admit, bool* ok = nullptr) {
+  if (ok) *ok = true;
   if (fd < 0) return -1;
   if (flock(fd, LOCK_EX) != 0) return -1;
   ShmEntry e[SHM_SLOTS];
@@ -606,19 +638,21 @@ int shm_exchange(int fd, int mine) {
     if (e[x].pid == me) {
       slot = x;
     } else if (e[x].pid > 0 && e[x].blocks > 0) {
-      if (kill(e[x].pid, 0) == 0 || errno == EPERM) {
+      if (shm_entry_live(e[x])) {
         others += e[x].blocks;
-      } else {  // a dead process's entry: free it
-        e[x] = ShmEntry{0, 0};
+      } else {  // a dead process's entry (or its pid reused): free it
+        e[x] = ShmEntry{0, 0, 0};
         dirty = true;
       }
     }
     if (free_slot < 0 && (e[x].pid <= 0 || e[x].blocks <= 0) && e[x].pid != me) free_slot = x;
   }
-  if (mine >= 0) {
+  const bool go = admit(others);
+  if (ok) *ok = go;
+  if (go && mine >= 0) {
     if (slot < 0) slot = free_slot;
     if (slot >= 0) {
-      e[slot] = ShmEntry{mine > 0 ? me : 0, mine};
+      e[slot] = mine > 0 ? ShmEntry{me, mine, proc_start(me)} : ShmEntry{0, 0, 0};
       dirty = true;
     }
   }
@@ -626,11 +660,14 @@ int shm_exchange(int fd, int mine) {
   flock(fd, LOCK_UN);
   return others;
 }
+int shm_set(int fd, int mine) {
+  return shm_exchange(fd, mine, [](int) { return true; });
+}
 
 ChainAdmission::~ChainAdmission() {
   // normal exit: this process's entries go back to the tables
   for (auto& kv : shm)
-    if (kv.second.fd >= 0 && kv.second.opener == getpid()) (void)shm_exchange(kv.second.fd, 0);
+    if (kv.second.fd >= 0 && kv.second.opener == getpid()) (void)shm_set(kv.second.fd, 0);
 }
 
 int adm_budget_locked(ChainAdmission& a, const spx_ctx* ctx) {
@@ -658,11 +695,12 @@ bool adm_acquire(spx_ctx* ctx) {
     // but their blocks count against the device's budget while they run, so
     // single-GPU chains beside them are refused instead of over-subscribing
     ok = ctx->sharded || used + extra <= cap;
-    if (ok && extra > 0) {  // the other processes' chains on this GPU (the shared table)
-      const int fd = shm_fd_locked(a, ctx->device);
-      const int others = shm_exchange(fd, -1);
-      ok = ctx->sharded || others < 0 || others + used + extra <= cap;
-      if (ok && fd >= 0) (void)shm_exchange(fd, used + extra);
+    if (ok && extra > 0) {  // the other processes' chains on this GPU (the shared table):
+      // read and claim under ONE flock, so two processes cannot both fit
+      const bool force = ctx->sharded;
+      const int want = used + extra;
+      (void)shm_exchange(shm_fd_locked(a, ctx->device), want,
+                         [&](int others) { return force || others + want <= cap; }, &ok);
     }
     if (ok) {
       used += extra;
@@ -682,7 +720,7 @@ void adm_release(spx_ctx* ctx) {
   if (ctx->adm_calls > 0 && --ctx->adm_calls == 0) {
     int& used = a.used[ctx->device];
     used -= ctx->adm_blocks;
-    if (ctx->adm_blocks > 0) (void)shm_exchange(shm_fd_locked(a, ctx->device), used);
+    if (ctx->adm_blocks > 0) (void)shm_set(shm_fd_locked(a, ctx->device), used);
     ctx->adm_blocks = 0;
   }
 }

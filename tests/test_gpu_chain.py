@@ -374,31 +374,41 @@ def test_chain_handshake_more_chains_than_cus_without_admission(eng_cls):
     print(f"windows rerun after a start-handshake abort: {sum(reruns)} ({reruns})")
 
 
+_SHM_ENTRY = "<iiQ"  # {pid, blocks, start time}: 16 B, 64 entries (spx_capi.hip ShmEntry)
+
+
 def _shm_entries(path):
     import fcntl
     import struct
     try:
         with open(path, "rb") as f:
             fcntl.flock(f, fcntl.LOCK_SH)
-            raw = f.read(512)
+            raw = f.read(1024)
     except FileNotFoundError:
         return []
-    raw = raw.ljust(512, b"\0")
-    return [struct.unpack_from("<ii", raw, 8 * x) for x in range(64)]
+    raw = raw.ljust(1024, b"\0")
+    return [struct.unpack_from(_SHM_ENTRY, raw, 16 * x)[:2] for x in range(64)]
 
 
-def _shm_put(path, pid, blocks):
-    """Write an entry {pid, blocks} into a free slot of the admission table,
-    under its flock (as another process's libspx would)."""
+def _proc_start(pid):
+    """Field 22 of /proc/<pid>/stat (what libspx records with an entry)."""
+    with open(f"/proc/{pid}/stat") as f:
+        return int(f.read().rsplit(")", 1)[1].split()[19])
+
+
+def _shm_put(path, pid, blocks, start=None):
+    """Write an entry {pid, blocks, start} into a free slot of the admission
+    table, under its flock (as another process's libspx would)."""
     import fcntl
     import struct
+    start = _proc_start(pid) if start is None else start
     fd = os.open(path, os.O_RDWR | os.O_CREAT, 0o666)
     try:
         fcntl.flock(fd, fcntl.LOCK_EX)
-        raw = os.pread(fd, 512, 0).ljust(512, b"\0")
-        ent = [struct.unpack_from("<ii", raw, 8 * x) for x in range(64)]
-        slot = next(x for x, (p, b) in enumerate(ent) if p <= 0 or b <= 0)
-        os.pwrite(fd, struct.pack("<ii", pid, blocks), 8 * slot)
+        raw = os.pread(fd, 1024, 0).ljust(1024, b"\0")
+        ent = [struct.unpack_from(_SHM_ENTRY, raw, 16 * x) for x in range(64)]
+        slot = next(x for x, (p, b, _) in enumerate(ent) if p <= 0 or b <= 0)
+        os.pwrite(fd, struct.pack(_SHM_ENTRY, pid, blocks, start), 16 * slot)
         fcntl.flock(fd, fcntl.LOCK_UN)
     finally:
         os.close(fd)
@@ -438,6 +448,13 @@ def test_chain_admission_shared_across_processes(eng_cls):
             e.solve(max_iters=48)
             assert e.chain_stats()["persistent_calls"] == 1
             assert not any(p == other.pid and b > 0 for p, b in _shm_entries(path))
+            # an entry whose pid is alive but belongs to another process (a
+            # reused pid: its start time differs) is stale too
+            _shm_put(path, os.getppid(), 200, start=_proc_start(os.getppid()) + 12345)
+            e.load(T, basis)
+            e.solve(max_iters=48)
+            assert e.chain_stats()["persistent_calls"] == 2
+            assert not any(p == os.getppid() and b > 0 for p, b in _shm_entries(path))
             e.run_pivots(4 * 24)  # no sync: released behind the launches, or at destroy
         assert not any(p == os.getpid() and b > 0 for p, b in _shm_entries(path))
     finally:
@@ -445,6 +462,52 @@ def test_chain_admission_shared_across_processes(eng_cls):
         if other.poll() is None:
             other.kill()
             other.wait()
+
+
+def test_chain_admission_two_real_processes(tmp_path):
+    """Two real libspx processes on GPU 0 (the reference's two gunicorn
+    workers, /root/reference/dockerfile:34) share the admission table.  Budget
+    24 blocks: the holder's 16-block chain is in flight (a long Bland run,
+    enqueued without a sync), so the asker's 16-block chain does not fit and
+    runs launch-per-phase; once the holder has exited, the asker's next call
+    is admitted.  Both results equal each other and the oracle's."""
+    import hashlib
+    import json
+    import subprocess
+    import sys
+    from simplex_amd import synth
+    worker = os.path.join(os.path.dirname(os.path.abspath(__file__)), "adm_worker.py")
+    sync = str(tmp_path)
+    env = dict(os.environ)
+    env.pop("SPX_CHAIN_SHM", None)
+    env.pop("SPX_CHAIN_BUDGET", None)
+    holder = subprocess.Popen([sys.executable, worker, "holder", sync, "24"], env=env,
+                              stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+    asker = subprocess.Popen([sys.executable, worker, "asker", sync, "24"], env=env,
+                             stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+    try:
+        hout, herr = holder.communicate(timeout=180)
+        assert holder.returncode == 0, herr[-2000:]
+        open(os.path.join(sync, "holder_done"), "w").close()
+        aout, aerr = asker.communicate(timeout=180)
+        assert asker.returncode == 0, aerr[-2000:]
+    finally:
+        for p_ in (holder, asker):
+            if p_.poll() is None:
+                p_.kill()
+                p_.wait()
+    h = json.loads(hout.strip().splitlines()[-1])
+    a = json.loads(aout.strip().splitlines()[-1])
+    assert h["stats"]["persistent_calls"] == 1, h
+    st1, st2 = a["stats"]
+    assert st1["refused_calls"] == 1 and st1["persistent_calls"] == 0, a
+    assert st2["persistent_calls"] == 1, a
+    assert a["iters"] == [48, 48] and a["digests"][0] == a["digests"][1]
+    T, basis = synth.full_tableau("degenerate", 2048, 2048, 5)
+    st, hist = O.solve_tableau(T, basis, rule="bland", max_iters=48)
+    assert hashlib.sha256(np.asarray(hist, dtype=np.int64).tobytes()).hexdigest() == \
+        a["digests"][0][0]
+    assert hashlib.sha256(T.tobytes()).hexdigest() == a["digests"][0][1]
 
 
 def test_chain_set_validated(eng_cls):
