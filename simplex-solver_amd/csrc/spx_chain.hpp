@@ -279,6 +279,11 @@ constexpr int GK_START = 3;  // a block's arrival at the start handshake (chain_
 // device groups also wait for every group's verdict: the window runs only
 // when all said GO.  Returns 0 go, 1 abort, 2 fault (a group never decided
 // within ~4 s).  Wave 0 only: the caller hands the result to its block.
+// a - b of two window epochs (TAG_EPOCH: 30 bits, wrapping), sign-extended
+__device__ __forceinline__ int32_t epoch_diff(uint32_t a, uint32_t b) {
+  return (int32_t)((a - b) << 2) >> 2;
+}
+
 template <bool SYS>
 __device__ __forceinline__ int chain_start(const gu64* arr, int nslots, int B, uint32_t gmask,
                                            gu64* vword, uint32_t W, int64_t bound,
@@ -299,7 +304,7 @@ __device__ __forceinline__ int chain_start(const gu64* arr, int nslots, int B, u
     const unsigned long long want = ((unsigned long long)W << 8) | (late ? 2u : 1u);
     unsigned long long cur = g_load<SYS>(vword);
     for (;;) {
-      const int32_t d = (int32_t)((uint32_t)(cur >> 8) - W);
+      const int32_t d = epoch_diff((uint32_t)(cur >> 8), W);
       if (d > 0) {  // the group is past W: W was aborted
         cur = 2u;
         break;
@@ -325,7 +330,7 @@ __device__ __forceinline__ int chain_start(const gu64* arr, int nslots, int B, u
       const gu64* w = (const gu64*)pe->ratio[pe->gleader[lane]] +
                       (size_t)(HS_PLANE_SHARD + 1) * CHAIN_SH_SLOTS;
       const unsigned long long x = g_load<true>(w);
-      const int32_t d = (int32_t)((uint32_t)(x >> 8) - W);
+      const int32_t d = epoch_diff((uint32_t)(x >> 8), W);
       dec = d >= 0;
       ab = d > 0 || (d == 0 && (x & 0xffu) == 2u);
     }

@@ -328,9 +328,11 @@ def test_chain_handshake_forced_abort_reruns_bit_exact(eng_cls, mode):
             e.state()
         e.set_chain_handshake(0)  # automatic bound again: the next call runs persistent
         e.load(T, basis)
+        n1 = e.chain_reruns()
         r2 = e.solve(max_iters=70)
         assert r2.iters == 70 and e.history().tolist() == ref[1]
         assert e.chain_stats()["persistent_calls"] >= 1
+        assert e.chain_reruns() == n1  # every window ran persistent (no abort left behind)
 
 
 def test_chain_handshake_more_chains_than_cus_without_admission(eng_cls):
