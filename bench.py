@@ -349,6 +349,9 @@ def main():
 
     per_step = K if K else 1  # pivots per step (one tableau pass)
     n_warm, n_timed = args.warmup * per_step, args.steps * per_step
+    # ranks start their first window together: a shard chain waits at most
+    # 100 ms at its start handshake for the other ranks' blocks
+    barrier()
     eng.run_pivots(n_warm, **opts)
     eng.sync()
     eng.elim_timing(reset=True)
@@ -483,6 +486,7 @@ def main():
             # every pivot of the run (warmup, timed, chain timing) from the
             # slack basis: tests compare it with the oracle's fixture
             "pivots_total": int(len(hist)),
+            "chain_reruns": int(eng.chain_reruns()) if hasattr(eng, "chain_reruns") else None,
             "pivots_sha256": hashlib.sha256(
                 np.ascontiguousarray(hist, dtype="<i8").tobytes()).hexdigest(),
         }

@@ -176,8 +176,14 @@ int spx_pivot_at(spx_ctx* ctx, int64_t r, int64_t c);
  * (benchmark primitive; pivots after termination are no-ops on the device).
  * If `time_elim` = k > 0, HIP events bracket every k-th elimination launch, or
  * in window mode every k-th window's flush; the timed launches are direct, the
- * other windows replay the per-window hipGraph when use_graph is set. */
+ * other windows replay the per-window hipGraph when use_graph is set.  A
+ * window whose persistent chain aborted at its start handshake (see
+ * spx_set_chain_handshake) is rerun by the next drain of the context
+ * (spx_sync, spx_state, a getter, or the next call), so the request still
+ * ends after exactly `npivots` pivots. */
 int spx_run_pivots(spx_ctx* ctx, const spx_opts* opts, int64_t npivots, int time_elim);
+/* Wait for the context's enqueued work (and finish an spx_run_pivots request
+ * whose window had to be rerun). */
 int spx_sync(spx_ctx* ctx);
 /* Device-side state after spx_sync: status code (SPX_RUNNING while going),
  * total pivots since load, and the objective-row RHS. */

@@ -167,6 +167,7 @@ struct spx_ctx {
   // after a chain found its blocks not co-resident (ST_NOTRES)
   int64_t hs_us = 0;
   int64_t chain_reruns = 0;
+  int64_t rp_target = -1;  // iterations the outstanding spx_run_pivots request ends at (-1: none)
 
   // graph cache
   // captured launch sequences by chunk (pivots): a few sizes per context
@@ -973,7 +974,12 @@ int set_state_fields(spx_ctx* ctx, int32_t status, int64_t fc, int64_t fr) {
   return SPX_OK;
 }
 
+int rp_recover(spx_ctx* ctx);
 int pull_state(spx_ctx* ctx) {
+  if (ctx->rp_target >= 0) {  // an spx_run_pivots request may need its rerun first
+    const int rc = rp_recover(ctx);
+    if (rc) return rc;
+  }
   HIPC(hipMemcpyAsync(ctx->h_st, ctx->st, sizeof(State), hipMemcpyDeviceToHost, ctx->stream));
   HIPC(hipStreamSynchronize(ctx->stream));
   return SPX_OK;
@@ -1055,7 +1061,7 @@ bool is_fault(int32_t st) { return st == ST_FAULT || st == ST_NOTRES; }
 int fault(spx_ctx* ctx) {
   if (ctx->h_st->status == ST_NOTRES)
     ctx->err = "a persistent chain's blocks were not co-resident, so its window did not run "
-               "(spx_run_pivots does not rerun it; spx_solve / spx_pivot do)";
+               "and could not be rerun";
   else
     ctx->err = "device fault: a pivot-chain exchange timed out";
   return SPX_E_STATE;
@@ -1090,6 +1096,32 @@ int notres_resume(spx_ctx* ctx, int64_t fc, int64_t fr, int* retries) {
     drop_graphs(ctx);
   }
   return set_state_fields(ctx, ST_RUNNING, fc, fr);
+}
+
+// An spx_run_pivots request does not wait for its launches, so it cannot
+// rerun a window whose persistent chain aborted at its start handshake
+// (ST_NOTRES: that window and the rest of the request did nothing).  The
+// points that drain the stream (spx_sync, spx_state, the getters, the next
+// call) finish it instead: the missing pivots run with the launch-per-phase
+// chain (a peer-only shard: the persistent chain again), as spx_solve's own
+// rerun does, so the request ends where it would have.
+int rp_recover(spx_ctx* ctx) {
+  if (ctx->rp_target < 0) return SPX_OK;
+  const int64_t target = ctx->rp_target;
+  ctx->rp_target = -1;
+  int retries = 0;
+  for (;;) {
+    HIPC(hipMemcpyAsync(ctx->h_st, ctx->st, sizeof(State), hipMemcpyDeviceToHost, ctx->stream));
+    HIPC(hipStreamSynchronize(ctx->stream));
+    if (ctx->h_st->status != ST_NOTRES || ctx->h_st->iters >= target) return SPX_OK;
+    int rc = notres_resume(ctx, -1, -1, &retries);
+    for (int64_t left = target - ctx->h_st->iters; !rc && left > 0;) {
+      const int n = (int)std::min<int64_t>(left, 1 << 20);
+      rc = enqueue_pivots(ctx, n, 0);
+      left -= n;
+    }
+    if (rc) return rc;
+  }
 }
 
 int alloc_common(spx_ctx* ctx, int64_t m_local, int64_t N, int64_t m_global, int64_t row0) {
@@ -1637,6 +1669,7 @@ int spx_set_objective(spx_ctx* ctx, const double* obj) {
 
 int spx_get_tableau(spx_ctx* ctx, double* out, int64_t ld, int layout) {
   if (!ctx) return SPX_E_ARG;
+  if (int rc = rp_recover(ctx)) return rc;
   CHECK_ARG(ctx->loaded && out, "no tableau / null buffer");
   CHECK_ARG(layout == SPX_ROW_MAJOR || layout == SPX_COL_MAJOR, "bad layout");
   const int64_t rows = ctx->m_local + 1, N = ctx->N;
@@ -1661,6 +1694,7 @@ int spx_get_tableau(spx_ctx* ctx, double* out, int64_t ld, int layout) {
 
 int spx_get_objective(spx_ctx* ctx, double* out) {
   if (!ctx) return SPX_E_ARG;
+  if (int rc = rp_recover(ctx)) return rc;
   CHECK_ARG(ctx->loaded && out, "no tableau / null buffer");
   HIPC(hipMemcpyAsync(out, ctx->obj, sizeof(double) * ctx->N, hipMemcpyDeviceToHost,
                       ctx->stream));
@@ -1670,6 +1704,7 @@ int spx_get_objective(spx_ctx* ctx, double* out) {
 
 int spx_get_basis(spx_ctx* ctx, int64_t* out) {
   if (!ctx) return SPX_E_ARG;
+  if (int rc = rp_recover(ctx)) return rc;
   CHECK_ARG(ctx->loaded && out, "no tableau / null buffer");
   if (ctx->m_global > 0) {
     HIPC(hipMemcpyAsync(out, ctx->basis, sizeof(int64_t) * ctx->m_global, hipMemcpyDeviceToHost,
@@ -1681,6 +1716,7 @@ int spx_get_basis(spx_ctx* ctx, int64_t* out) {
 
 int spx_get_column(spx_ctx* ctx, int64_t j, double* out) {
   if (!ctx) return SPX_E_ARG;
+  if (int rc = rp_recover(ctx)) return rc;
   CHECK_ARG(ctx->loaded && out && j >= 0 && j < ctx->N, "bad column");
   if (ctx->m_local > 0) {
     HIPC(hipMemcpyAsync(out, ctx->A + j * ctx->ld, sizeof(double) * ctx->m_local,
@@ -1852,6 +1888,7 @@ int spx_run_pivots(spx_ctx* ctx, const spx_opts* opts, int64_t npivots, int time
   AdmCall adm_call(ctx);  // released behind this call's launches (it does not sync)
   int rc = begin_call(ctx, o, &adm_call);
   if (rc) return rc;
+  ctx->rp_target = ctx->h_st->iters + npivots;  // (begin_call drained: iters is current)
   // (chain timing records one event pair per window: direct launches, since a
   // replayed graph re-records the same captured events)
   const bool graph = o->use_graph && !ctx->loop && !ctx->time_chain;
@@ -1950,7 +1987,7 @@ int spx_set_window(spx_ctx* ctx, int K) {
 int spx_sync(spx_ctx* ctx) {
   if (!ctx) return SPX_E_ARG;
   HIPC(hipStreamSynchronize(ctx->stream));
-  return SPX_OK;
+  return rp_recover(ctx);
 }
 
 int spx_state(spx_ctx* ctx, int32_t* status, int64_t* iters, double* objective) {
@@ -2045,6 +2082,7 @@ int spx_set_elim_variant(spx_ctx* ctx, int R, int target_wgs, int nt_flags, int 
 
 int spx_get_row(spx_ctx* ctx, int64_t i, double* out) {
   if (!ctx) return SPX_E_ARG;
+  if (int rc = rp_recover(ctx)) return rc;
   CHECK_ARG(ctx->loaded && out && i >= 0 && i < ctx->m_local, "bad row");
   HIPC(hipSetDevice(ctx->device));
   double* d = nullptr;

@@ -298,8 +298,8 @@ def test_chain_handshake_forced_abort_reruns_bit_exact(eng_cls, mode):
     start handshake (ST_NOTRES) before any block stores anything; spx_solve,
     spx_pivot and spx_pivot_at rerun the aborted window with the
     launch-per-phase chain, so the bytes equal a plain run's and the oracle's.
-    spx_run_pivots cannot rerun: its abort surfaces at spx_state."""
-    from simplex_amd.engine import SpxError
+    spx_run_pivots does not wait for its launches: the drain that follows it
+    (spx_sync, spx_state, a getter) runs the missing pivots instead."""
     T, basis = _random_tableau(300, 900, seed=71)
     ref = _run(eng_cls, T, basis, 16, mode, max_iters=70)
     Tc, bc = T.copy(), basis.copy()
@@ -322,10 +322,19 @@ def test_chain_handshake_forced_abort_reruns_bit_exact(eng_cls, mode):
         e.pivot_at(5, fc)
         assert e.chain_reruns() >= n0 + 2
         assert np.array_equal(e.tableau(), Tc) and np.array_equal(e.basis(), bc)
-        e.run_pivots(16)
+        n2 = e.chain_reruns()
+        e.run_pivots(40)
         e.sync()
-        with pytest.raises(SpxError, match="not co-resident"):
-            e.state()
+        assert e.chain_reruns() == n2 + 1
+        st, it, _ = e.state()
+        assert it == 70 + 2 + 40
+        O.solve_tableau(Tc, bc, max_iters=40)
+        assert np.array_equal(e.tableau(), Tc) and np.array_equal(e.basis(), bc)
+        e.run_pivots(16)  # no explicit sync: the next call's drain finishes it
+        e.pivot()
+        O.solve_tableau(Tc, bc, max_iters=17)
+        assert e.state()[1] == 70 + 2 + 40 + 17
+        assert np.array_equal(e.tableau(), Tc) and np.array_equal(e.basis(), bc)
         e.set_chain_handshake(0)  # automatic bound again: the next call runs persistent
         e.load(T, basis)
         n1 = e.chain_reruns()
