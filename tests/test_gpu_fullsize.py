@@ -39,7 +39,7 @@ def _digest(T):
     return hashlib.sha256(np.ascontiguousarray(T).tobytes()).hexdigest()
 
 
-def _full_solve(name, window=24):
+def _full_solve(name, window=24, chain=0):
     """The fixture's solve on the GPU: to optimality, or over the fixture's
     pivot prefix (max_pivots, status 1) when the oracle run was capped."""
     from simplex_amd import synth
@@ -49,8 +49,11 @@ def _full_solve(name, window=24):
     Tf, obj, basis = synth.tableau_rows(fx["kind"], fx["m"], fx["n"], fx["seed"], order="F")
     with DeviceTableau(0) as e:
         e.set_window(window)
+        e.set_chain(chain)
         e.load_rows(Tf, obj, basis, fx["m"], 0)
         del Tf
+        if chain >= 4:
+            assert e.chain_blocks() == (32 if chain == 4 else 64)
         done = 0
         for k in sorted(int(x) for x in fx["checkpoint_sha256"]):
             r = e.solve(rule=fx["rule"], max_iters=k - done)
@@ -72,12 +75,14 @@ def _full_solve(name, window=24):
     return fx
 
 
-@pytest.mark.parametrize("window", [24, 28])
-def test_config3_dantzig_full_solve_pinned(window):
+@pytest.mark.parametrize("window,chain", [(24, 0), (28, 0), (24, 4), (24, 5)],
+                         ids=["k24", "k28", "k24-xcd512", "k24-xcd256"])
+def test_config3_dantzig_full_solve_pinned(window, chain):
     """Config 3 (8192 x 8192 dense LP, tableau 8193 x 16385): the whole
-    Dantzig solve at K = 24 and at the bench's K = 28 vs the oracle's, index
-    for index."""
-    _full_solve("config3", window=window)
+    Dantzig solve at K = 24 and 28, and with the one-XCD chain forms (modes 4
+    and 5, whose row gather synthesizes the basic columns' values), vs the
+    oracle's, index for index."""
+    _full_solve("config3", window=window, chain=chain)
 
 
 def test_config5_bland_100k_pivots_pinned():
