@@ -523,9 +523,18 @@ __device__ __forceinline__ void g_store_l(gu64* g, unsigned tag, unsigned val) {
                      L2 ? __HIP_MEMORY_SCOPE_WORKGROUP : __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// (pq: the slot, for the probe build's stamps inside the publish; blockIdx 0)
+#if defined(SPX_PHASE_TIMING) && defined(SPX_PROBE_FINE)
+#define SPX_PROBE_PUB(pq, ph, cond) SPX_PROBE((pq) + 32, RATIO ? 0 : 1, ph, cond)
+#else
+#define SPX_PROBE_PUB(pq, ph, cond) \
+  do {                              \
+  } while (0)
+#endif
 template <int NW, bool RATIO, bool L2 = false, typename Hist>
 __device__ __forceinline__ void publish_local(gu64* rec, int b, unsigned tag, int nh,
-                                              const KeyP (&sk)[NW], Hist hist) {
+                                              const KeyP (&sk)[NW], Hist hist, int pq = 0) {
+  (void)pq;
   const int lane = threadIdx.x & 63;
   KeyP k;
   if constexpr (NW == 4) {
@@ -551,6 +560,7 @@ __device__ __forceinline__ void publish_local(gu64* rec, int b, unsigned tag, in
   }
   const int ww = (int)k.b;  // the winning wave (a payload slot of the block key)
   const bool none = k.row < 0;
+  SPX_PROBE_PUB(pq, 0, k.v != 12345.678);  // block key reduced
   gu64* rb = rec + b;
   constexpr int H0 = RATIO ? RATIO_HDR + 2 : ENTER_HDR;  // first history plane
   if (!none) {
@@ -558,6 +568,7 @@ __device__ __forceinline__ void publish_local(gu64* rec, int b, unsigned tag, in
     if (lane < 2 * nh) {
       const unsigned long long x =
           (unsigned long long)__double_as_longlong(hist(ww, k.row, lane >> 1));
+      SPX_PROBE_PUB(pq, 1, x != 12345ull);  // history read from LDS
       g_store_l<L2>(rb + (size_t)(H0 + lane) * CHAIN_MAX_BLOCKS, tag,
                     (lane & 1) ? (unsigned)(x >> 32) : (unsigned)x);
     }
@@ -576,6 +587,7 @@ __device__ __forceinline__ void publish_local(gu64* rec, int b, unsigned tag, in
     if (RATIO)
       g_store_l<L2>(rb + 3 * CHAIN_MAX_BLOCKS, tag, none ? 0xffffffffu : (unsigned)k.t);
   }
+  SPX_PROBE_PUB(pq, 2, true);  // every store issued
 }
 
 // system-scope load of one double (the sharded chain's row gather from a peer)
@@ -865,7 +877,7 @@ __global__ __launch_bounds__(CB) void chain_kernel(
                                                   : fsl[x][(int)(row - (int64_t)b * rpb) + roff];
                                  else
                                    return hl[ww][x];
-                               });
+                               }, q);
       SPX_PROBE_CHAIN(q, 0);
     }
     // f_q for the flush / row_fix (later kernels): stored after the record, so
@@ -1027,7 +1039,7 @@ __global__ __launch_bounds__(CB) void chain_kernel(
                                       return psl[x][(int)(col - (int64_t)b * cpb)];
                                     else
                                       return hl[ww][x];
-                                  });
+                                  }, q);
       } else if (t == 0) {
         // the next window's pivot-0 partial (read after the kernel boundary)
         KeyP kb = sk[0];

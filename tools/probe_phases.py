@@ -80,6 +80,10 @@ def main():
                 print(f"       fine: loads arrived +{a0 - ph[1]:5.2f}  slots applied "
                       f"+{a1 - a0:5.2f}  rest of phase2 +{ph[2] - a1:5.2f}  | end: argmin+lds "
                       f"+{a2 - ph[2]:5.2f}  barrier +{a3 - a2:5.2f}  publish +{ph[3] - a3:5.2f}")
+                if t(q + 32, kind, 2) > t0:  # stamps inside the publish (SPX_PROBE_FINE)
+                    p0, p1, p2 = (us(t(q + 32, kind, x)) for x in range(3))
+                    print(f"       publish: key reduced +{p0 - a3:5.2f}  history read "
+                          f"+{p1 - p0:5.2f}  stores issued +{p2 - p1:5.2f}  rest +{ph[3] - p2:5.2f}")
             if kind == 0 and os.environ.get("SPX_PROBE_FINE"):
                 k0, k1 = us(t(q, 2, 0)), us(t(q, 2, 1))
                 print(f"       fine: keys reduced +{k0 - ph[0]:5.2f}  wave_min +{k1 - k0:5.2f}")
