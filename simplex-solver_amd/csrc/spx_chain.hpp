@@ -248,6 +248,28 @@ __device__ __forceinline__ KeyP key_of_lane(const KeyP& k, int ln) {
               rdlane(k.b, ln)};
 }
 
+// The block's key from its 4 wave keys (lanes 0..3 hold them, lexicographic
+// (v, t) as kmin2): a quad DPP min of v, the tied lanes by ballot, and --
+// unless t grows with the lane (mono) -- a quad DPP min of t among them; then
+// the winner's fields read once.  Fewer dependent steps than two kmin2_dpp
+// rounds (10 DPP moves and a branchy compare each) plus key_of_lane.
+__device__ __forceinline__ KeyP block_key4(const KeyP& mine, bool mono) {
+  const int lane = threadIdx.x & 63;
+  double m = mine.v;
+  m = dpp_minf<0xB1>(m);  // quad_perm [1,0,3,2]
+  m = dpp_minf<0x4E>(m);  // quad_perm [2,3,0,1]
+  const double vmin = rdlane(m, 0);
+  uint64_t tie = __ballot(lane < 4 && mine.v == vmin) & 0xfull;
+  if (!mono && __popcll(tie) > 1) {
+    int64_t x = ((tie >> lane) & 1ull) ? mine.t : INT64_MAX;
+    x = dpp_mini<0xB1>(x);
+    x = dpp_mini<0x4E>(x);
+    const int64_t tmin = rdlane64(x, 0);
+    tie &= __ballot(((tie >> lane) & 1ull) && mine.t == tmin);
+  }
+  return key_of_lane(mine, tie ? (int)__builtin_ctzll(tie) : 0);
+}
+
 // Bounded spin bookkeeping: true (and ST_FAULT stored) once a wait ran too long.
 __device__ __forceinline__ bool spin_fail(unsigned& spins, State* st) {
   if (++spins < CHAIN_SPIN_MAX) {
@@ -457,9 +479,15 @@ __device__ __forceinline__ bool load_extras(const gu64* rec, int wb, int h0, int
 template <int NW, bool RATIO, bool SYS = false, int rs = CHAIN_MAX_BLOCKS, typename Dst, typename Hist>
 __device__ __forceinline__ void publish_record(Dst dst, int nd, unsigned tag, int nh,
                                                const KeyP (&sk)[NW], Hist hist,
-                                               unsigned stopbit = 0u) {
+                                               unsigned stopbit = 0u, bool mono = false) {
   const int lane = threadIdx.x & 63;
   KeyP k;
+  (void)mono;
+#ifdef SPX_KEY4_SHARD
+  if constexpr (NW == 4) {
+    k = block_key4(lane < NW ? sk[lane] : keyp_none(), mono);
+  } else
+#endif
   if constexpr (NW == 4) {
     // one LDS read (lane x < 4 takes wave x's key) and two quad DPP steps,
     // instead of four dependent broadcast reads and compares
@@ -533,17 +561,17 @@ __device__ __forceinline__ void g_store_l(gu64* g, unsigned tag, unsigned val) {
 #endif
 template <int NW, bool RATIO, bool L2 = false, typename Hist>
 __device__ __forceinline__ void publish_local(gu64* rec, int b, unsigned tag, int nh,
-                                              const KeyP (&sk)[NW], Hist hist, int pq = 0) {
+                                              const KeyP (&sk)[NW], Hist hist, int pq = 0,
+                                              bool mono = false) {
   (void)pq;
   const int lane = threadIdx.x & 63;
   KeyP k;
   if constexpr (NW == 4) {
-    // one LDS read (lane x < 4 takes wave x's key) and two quad DPP steps,
-    // instead of four dependent broadcast reads and compares
-    k = lane < NW ? sk[lane] : keyp_none();
-    kmin2_dpp<0xB1>(k);  // quad_perm [1,0,3,2]
-    kmin2_dpp<0x4E>(k);  // quad_perm [2,3,0,1]
-    k = key_of_lane(k, 0);
+    // one LDS read (lane x < 4 takes wave x's key), a quad DPP min of the
+    // values and the tied lanes by ballot (mono: t grows with the wave);
+    // two full kmin2_dpp rounds measured 0.13 us per pivot slower
+    // (profiles/r04/ab_block_key4.jsonl)
+    k = block_key4(lane < NW ? sk[lane] : keyp_none(), mono);
   } else if constexpr (NW == 8) {
     // lanes 0..7 hold the wave keys: the row-of-16 DPP reduction (rotations
     // by 8 and 4, then the quad steps) leaves lane 0 with their minimum
@@ -877,7 +905,7 @@ __global__ __launch_bounds__(CB) void chain_kernel(
                                                   : fsl[x][(int)(row - (int64_t)b * rpb) + roff];
                                  else
                                    return hl[ww][x];
-                               }, q);
+                               }, q, rule != RULE_BLAND);
       SPX_PROBE_CHAIN(q, 0);
     }
     // f_q for the flush / row_fix (later kernels): stored after the record, so
@@ -1039,7 +1067,7 @@ __global__ __launch_bounds__(CB) void chain_kernel(
                                       return psl[x][(int)(col - (int64_t)b * cpb)];
                                     else
                                       return hl[ww][x];
-                                  }, q);
+                                  }, q, true);
       } else if (t == 0) {
         // the next window's pivot-0 partial (read after the kernel boundary)
         KeyP kb = sk[0];
@@ -2009,7 +2037,7 @@ __global__ __launch_bounds__(CB) void chain_shard_kernel(
                                      else
                                        return hl[ww][x];
                                    },
-                                   stopbit);
+                                   stopbit, rule != RULE_BLAND);
       SPX_PROBE_CHAIN(q, 0);
     }
     // f_q for the flush / row_fix (later kernels): stored after the record, so
@@ -2179,7 +2207,7 @@ __global__ __launch_bounds__(CB) void chain_shard_kernel(
                                       return psl[x][(int)(col - (int64_t)b * cpb)];
                                     else
                                       return hl[ww][x];
-                                  });
+                                  }, 0u, true);
       } else if (t == 0) {
         // the next window's pivot-0 partial (read after the kernel boundary)
         KeyP kb = sk[0];
