@@ -482,19 +482,10 @@ __device__ __forceinline__ void publish_record(Dst dst, int nd, unsigned tag, in
                                                unsigned stopbit = 0u, bool mono = false) {
   const int lane = threadIdx.x & 63;
   KeyP k;
-  (void)mono;
-#ifdef SPX_KEY4_SHARD
   if constexpr (NW == 4) {
+    // one LDS read (lane x < 4 takes wave x's key), a quad DPP min and the
+    // tied lanes by ballot (block_key4; as publish_local)
     k = block_key4(lane < NW ? sk[lane] : keyp_none(), mono);
-  } else
-#endif
-  if constexpr (NW == 4) {
-    // one LDS read (lane x < 4 takes wave x's key) and two quad DPP steps,
-    // instead of four dependent broadcast reads and compares
-    k = lane < NW ? sk[lane] : keyp_none();
-    kmin2_dpp<0xB1>(k);  // quad_perm [1,0,3,2]
-    kmin2_dpp<0x4E>(k);  // quad_perm [2,3,0,1]
-    k = key_of_lane(k, 0);
   } else {
     k = sk[0];
 #pragma unroll
