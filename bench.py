@@ -133,6 +133,12 @@ def cpu_baseline(m, n, seed, rule, budget_s, gpu_hist):
     k, el = c_run(threads, budget_s * 0.6, Tc, bc, hist)
     # 1 thread, continuing the same sequence
     k1, el1 = c_run(1, budget_s * 0.2, Tc, bc, hist)
+    # the thread-scaling curve between them (short samples, same sequence)
+    scaling = {"1": k1 / el1 if el1 > 0 else None, str(threads): k / el}
+    for tt in (2, 4, 8):
+        if tt < threads:
+            kt, elt = c_run(tt, budget_s * 0.06, Tc, bc, hist)
+            scaling[str(tt)] = kt / elt if elt > 0 and kt else None
     C.set_threads(threads)
     del Tc
     ok = matches(hist)
@@ -157,7 +163,8 @@ def cpu_baseline(m, n, seed, rule, budget_s, gpu_hist):
                           "seconds": el1},
             "numpy_1thread": {"value": k2 / el2, "pivots": k2, "seconds": el2,
                               "matches_gpu": bool(ok2)},
-            "all_cores": _all_cores_projection(k / el, threads, host, alg_bytes_per_pivot(m, n)),
+            "all_cores": _all_cores_projection(k / el, threads, host, alg_bytes_per_pivot(m, n),
+                                               scaling),
             "host": host}
 
 
@@ -172,13 +179,15 @@ def alg_bytes_per_pivot(m, n):
     return 16.0 * m * (n + 1)
 
 
-def _all_cores_projection(v, threads, host, bytes_per_pivot):
+def _all_cores_projection(v, threads, host, bytes_per_pivot, scaling=None):
     """The C oracle on every physical core is NOT run: the harness gives this
     job 16 threads (OMP_NUM_THREADS=16 on the box, the other cores belong to
-    other jobs).  What is reported instead is an upper bound: the measured
-    rate scaled linearly to all physical cores, capped by the host's DRAM
-    roofline (sockets x spec bandwidth / bytes per pivot) -- the CPU path is
-    as memory-bound as the GPU's."""
+    other jobs).  What is reported instead: the measured thread-scaling curve
+    (1 .. `threads`), the rate scaled linearly to all physical cores, the
+    rate extrapolated at the last measured doubling's efficiency, and the
+    host's DRAM roofline (sockets x spec bandwidth / bytes per pivot) -- the
+    CPU path is as memory-bound as the GPU's.  upper_bound = min(linear,
+    roofline); estimate = min(doubling extrapolation, roofline)."""
     phys = host.get("physical_cores")
     model = host.get("model") or ""
     per_socket = next((bw for k, bw in HOST_DRAM_PEAK.items() if k in model), None)
@@ -186,9 +195,16 @@ def _all_cores_projection(v, threads, host, bytes_per_pivot):
     lin = v * phys / threads if phys and threads else None
     roof = peak * 1e9 / bytes_per_pivot if peak else None
     cands = [x for x in (lin, roof) if x]
+    est = None
+    half = (scaling or {}).get(str(threads // 2))
+    if phys and threads and half and v > half and phys > threads:
+        import math
+        est = v * (v / half) ** math.log2(phys / threads)  # each further doubling at that gain
+        est = min(est, roof) if roof else est
     return {"measured": False,
             "why": "the harness caps this job at 16 host threads (OMP_NUM_THREADS=16)",
-            "physical_cores": phys, "linear_projection": lin,
+            "physical_cores": phys, "measured_scaling": scaling,
+            "linear_projection": lin, "doubling_extrapolation": est,
             "host_dram_peak_GBps": peak, "dram_roofline_pivots_per_s": roof,
             "upper_bound": min(cands) if cands else None}
 

@@ -292,3 +292,26 @@ def test_storage_report_mode_and_unwritable_dir(tmp_path, monkeypatch):
     blocker.write_text("x")
     monkeypatch.setattr(storage, "OUTPUT_DIR", str(blocker / "sub"))
     assert storage.StorageService.save_solution({"a": 1}) is None
+
+
+def test_bench_all_cores_projection_bounds():
+    """bench.py's all-physical-cores CPU figure (not measured: the harness
+    gives the job 16 threads): linear scaling of the 16-thread rate, the
+    last doubling's gain carried on, both capped by the host's DRAM roofline
+    for the bytes one pivot moves."""
+    import bench
+    host = {"physical_cores": 128, "model": "AMD EPYC 9575F 64-Core Processor", "sockets": 2}
+    bpp = bench.alg_bytes_per_pivot(8192, 8192)
+    assert bpp == 16.0 * 8192 * 8193
+    curve = {"1": 20.0, "2": 39.0, "4": 75.0, "8": 130.0, "16": 205.0}
+    a = bench._all_cores_projection(205.0, 16, host, bpp, curve)
+    roof = 2 * 614.4e9 / bpp
+    assert a["measured"] is False and a["measured_scaling"] == curve
+    assert abs(a["linear_projection"] - 205.0 * 8) < 1e-9
+    assert abs(a["dram_roofline_pivots_per_s"] - roof) < 1e-6
+    assert a["upper_bound"] == min(a["linear_projection"], roof)
+    # three more doublings at 205/130 each, under the roofline here
+    assert abs(a["doubling_extrapolation"] - min(205.0 * (205.0 / 130.0) ** 3, roof)) < 1e-6
+    # unknown host model: no roofline, the linear figure bounds it
+    b = bench._all_cores_projection(205.0, 16, dict(host, model="other"), bpp, curve)
+    assert b["dram_roofline_pivots_per_s"] is None and b["upper_bound"] == 205.0 * 8
