@@ -12,6 +12,7 @@ PYT="python -u -m pytest -x -v --timeout 300 --timeout-method thread"
 for s in ${STEPS:-probe tests bench}; do
   case $s in
     probe) TAILN=12 run 120 xcd_probe.log ./tools/xcd_exchange_probe 2000 ;;
+    stagger) TAILN=24 run 180 stagger_probe.log ./tools/poll_stagger_probe 2000 ;;
     tests) if [ -n "${KEXPR:-}" ]; then
              run 900 pytest_sel.log $PYT ${TESTS:-tests/test_gpu_chain.py tests/test_gpu_peer_chain.py} -k "$KEXPR"
            else
