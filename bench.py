@@ -168,6 +168,12 @@ def cpu_baseline(m, n, seed, rule, budget_s, gpu_hist):
             "host": host}
 
 
+# The pivot chain's latency floor per pivot (MI355X_MICROARCH.md price list,
+# idle chip): an in-launch all-gather of a few KB among 32-256 CUs, and one
+# dependent HBM miss.
+CHAIN_EXCHANGE_FLOOR_US = 2.4
+HBM_MISS_FLOOR_US = 0.4
+
 # Host DRAM peak by CPU model (spec): EPYC 9005 "Turin" sockets have 12 DDR5-6400
 # channels = 614.4 GB/s each.
 HOST_DRAM_PEAK = {"EPYC 9575F": 614.4}
@@ -409,6 +415,14 @@ def main():
                  "share_of_step": (c_ms / max(c_n, 1)) / (1e3 * elapsed / args.steps),
                  "window": f"HIP events around the chain of {c_n} windows run after the "
                            f"timed region"}
+        if nb:
+            # the chain's latency roofline: per pivot two in-launch
+            # all-to-all exchanges among the blocks and two dependent HBM gathers,
+            # at MI355X_MICROARCH.md's idle-chip prices (all-gather among 32-256
+            # CUs >= 2.4 us, a dependent HBM miss >= 0.4 us)
+            floor = 2 * CHAIN_EXCHANGE_FLOOR_US + 2 * HBM_MISS_FLOOR_US
+            chain["latency_floor_us_per_pivot"] = floor
+            chain["frac_of_floor"] = floor / chain["us_per_pivot"] if chain["us_per_pivot"] else None
     what = "flush (window pass)" if K else "elimination"
     between = every - 1
     every = f"every {every}th"
