@@ -168,6 +168,7 @@ struct spx_ctx {
   int64_t hs_us = 0;
   int64_t chain_reruns = 0;
   int64_t rp_target = -1;  // iterations the outstanding spx_run_pivots request ends at (-1: none)
+  bool st_fresh = false;   // h_st equals the device State (pulled, nothing enqueued since)
 
   // graph cache
   // captured launch sequences by chunk (pivots): a few sizes per context
@@ -562,6 +563,18 @@ uint64_t proc_start(int32_t pid) {
   return field == 22 ? std::strtoull(p, nullptr, 10) : 0;
 }
 
+// This process's start time (read once; a fork()ed child reads its own).
+uint64_t my_start() {
+  static pid_t who = 0;
+  static uint64_t t = 0;
+  const pid_t me = getpid();
+  if (who != me) {
+    t = proc_start((int32_t)me);
+    who = me;
+  }
+  return t;
+}
+
 // Is the table entry's process alive (and the same process that wrote it)?
 bool shm_entry_live(const ShmEntry& e) {
   if (!(kill(e.pid, 0) == 0 || errno == EPERM)) return false;
@@ -653,7 +666,7 @@ int shm_exchange(int fd, int mine, Admit admit, bool* ok = nullptr) {
   if (go && mine >= 0) {
     if (slot < 0) slot = free_slot;
     if (slot >= 0) {
-      e[slot] = mine > 0 ? ShmEntry{me, mine, proc_start(me)} : ShmEntry{0, 0, 0};
+      e[slot] = mine > 0 ? ShmEntry{me, mine, my_start()} : ShmEntry{0, 0, 0};
       dirty = true;
     }
   }
@@ -937,19 +950,18 @@ int enqueue_pivots(spx_ctx* ctx, int npiv, int time_k, int64_t first = 0) {
   return SPX_OK;
 }
 
-int write_params(spx_ctx* ctx, const spx_opts* o) {
+int make_params(spx_ctx* ctx, const spx_opts* o, Params* out) {
   spx_opts d;
   spx_default_opts(&d);
   if (!o) o = &d;
   CHECK_ARG(o->rule == SPX_RULE_DANTZIG || o->rule == SPX_RULE_BLAND, "unknown pivot rule");
-  Params p;
+  Params& p = *out;
   p.rule = o->rule;
   p.skip_zero = o->skip_zero_cols ? 1 : 0;
   p.eps_opt = o->eps_opt;
   p.eps_piv = o->eps_piv;
   p.n_enter = (o->n_enter > 0) ? std::min<int64_t>(o->n_enter, ctx->N - 1) : ctx->N - 1;
   p.iter_limit = (o->max_iters > 0) ? ctx->h_st->iters + o->max_iters : INT64_MAX;
-  HIPC(hipMemcpyAsync(ctx->prm, &p, sizeof(p), hipMemcpyHostToDevice, ctx->stream));
   return SPX_OK;
 }
 
@@ -980,8 +992,10 @@ int pull_state(spx_ctx* ctx) {
     const int rc = rp_recover(ctx);
     if (rc) return rc;
   }
+  ctx->st_fresh = false;
   HIPC(hipMemcpyAsync(ctx->h_st, ctx->st, sizeof(State), hipMemcpyDeviceToHost, ctx->stream));
   HIPC(hipStreamSynchronize(ctx->stream));
+  ctx->st_fresh = true;
   return SPX_OK;
 }
 
@@ -995,19 +1009,26 @@ int begin_call(spx_ctx* ctx, const spx_opts* o, AdmCall* adm_call, int64_t fc = 
   }
   HIPC(hipSetDevice(ctx->device));
   (void)hipGetLastError();  // drop a stale error of an unrelated earlier call
-  int rc = pull_state(ctx);
-  if (rc) return rc;
+  int rc = SPX_OK;
+  // the host's State copy must be current (iters, status); a pull is a
+  // stream round trip, skipped when nothing was enqueued since the last one
+  if (!ctx->st_fresh && (rc = pull_state(ctx))) return rc;
   if (ctx->h_stop) __atomic_store_n(ctx->h_stop, 0, __ATOMIC_SEQ_CST);  // (stream drained above)
-  if ((rc = write_params(ctx, o))) return rc;
-  if ((rc = set_state_fields(ctx, ST_RUNNING, fc, fr))) return rc;
+  Params p;
+  if ((rc = make_params(ctx, o, &p))) return rc;
+  ctx->st_fresh = false;  // (from here on the device State moves on)
+  ctx->h_st->status = ST_RUNNING;
+  ctx->h_st->forced_c = fc;
+  ctx->h_st->forced_r = fr;
+  ctx->h_st->hs_ticks = hs_ticks(ctx);
+  // params + State fields (+ the window kernels' entering partials past the
+  // nbn that INIT writes) in one launch
+  const int n = ctx->win_k ? enter_part_len(ctx) - ctx->nbn : 0;
+  hipLaunchKernelGGL(call_begin_kernel, dim3(std::max(1, (n + BLK - 1) / BLK)), dim3(BLK), 0,
+                     ctx->stream, ctx->prm, p, ctx->st, (int32_t)ST_RUNNING, fc, fr,
+                     ctx->h_st->hs_ticks, ctx->enter_part + ctx->nbn, n);
   launch_norm<MODE_INIT>(ctx);
-  if (!ctx->win_k) {
-    launch_prime(ctx);
-  } else {  // the window kernels reduce up to enter_part_len partials; INIT wrote the first nbn
-    const int n = enter_part_len(ctx) - ctx->nbn;
-    hipLaunchKernelGGL(fill_none_kernel, dim3((n + BLK - 1) / BLK), dim3(BLK), 0, ctx->stream,
-                       ctx->enter_part + ctx->nbn, n);
-  }
+  if (!ctx->win_k) launch_prime(ctx);
   HIPC(hipGetLastError());
   adm_call->held = adm_acquire(ctx);  // persistent or launch-per-phase chain for this call
   return SPX_OK;
@@ -1113,7 +1134,11 @@ int rp_recover(spx_ctx* ctx) {
   for (;;) {
     HIPC(hipMemcpyAsync(ctx->h_st, ctx->st, sizeof(State), hipMemcpyDeviceToHost, ctx->stream));
     HIPC(hipStreamSynchronize(ctx->stream));
-    if (ctx->h_st->status != ST_NOTRES || ctx->h_st->iters >= target) return SPX_OK;
+    if (ctx->h_st->status != ST_NOTRES || ctx->h_st->iters >= target) {
+      ctx->st_fresh = true;
+      return SPX_OK;
+    }
+    ctx->st_fresh = false;
     int rc = notres_resume(ctx, -1, -1, &retries);
     for (int64_t left = target - ctx->h_st->iters; !rc && left > 0;) {
       const int n = (int)std::min<int64_t>(left, 1 << 20);
@@ -1204,6 +1229,7 @@ int alloc_common(spx_ctx* ctx, int64_t m_local, int64_t N, int64_t m_global, int
   ctx->h_st->forced_r = -1;
   ctx->h_st->hist_cap = ctx->hist_cap;
   HIPC(hipMemcpyAsync(ctx->st, ctx->h_st, sizeof(State), hipMemcpyHostToDevice, ctx->stream));
+  ctx->st_fresh = false;  // (the load's first call pulls once)
   return SPX_OK;
 }
 

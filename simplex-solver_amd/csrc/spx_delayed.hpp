@@ -189,6 +189,25 @@ __global__ __launch_bounds__(BLK) void fill_none_kernel(Key* __restrict__ k, int
   if (x < n) store_key(k + x, keyr_none());
 }
 
+// The start of a pivot call as ONE launch instead of two host copies on the
+// stream (each a copy-engine hand-off before the first kernel): the call's
+// parameters and the State fields the host sets -- status, forced pivot,
+// handshake bound -- plus fill_none_kernel's n keys (windowed calls).
+__global__ __launch_bounds__(BLK) void call_begin_kernel(Params* __restrict__ prm, Params p,
+                                                         State* __restrict__ st, int32_t status,
+                                                         int64_t fc, int64_t fr, int64_t hs,
+                                                         Key* __restrict__ k, int n) {
+  const int x = blockIdx.x * BLK + threadIdx.x;
+  if (x == 0) {
+    *prm = p;
+    st->status = status;
+    st->forced_c = fc;
+    st->forced_r = fr;
+    st->hs_ticks = hs;
+  }
+  if (x < n) store_key(k + x, keyr_none());
+}
+
 // ---------------------------------------------------------------------------
 // lazy_ratio_kernel<KMAX> (slot q < KMAX = number of pending pivots): entering
 // column of the coming pivot (or forced), its current values -> F[q], min-ratio
