@@ -32,6 +32,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <map>
+#include <set>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -150,6 +151,8 @@ struct spx_ctx {
   // was refused (its windows then run the launch-per-phase chain)
   int adm_blocks = 0;
   int adm_calls = 0;
+  int adm_deferred = 0;          // calls whose reservation waits for adm_ev (adm_settle)
+  hipEvent_t adm_ev = nullptr;   // recorded behind the last such call's launches
   bool chain_denied = false;
   int64_t chain_calls[2] = {0, 0};  // calls run with the persistent / the lazy chain
 
@@ -602,6 +605,7 @@ struct ChainAdmission {
   std::map<int, int> used;    // chain blocks in flight, by device
   std::map<int, int> budget;  // explicit budgets (spx_set_chain_budget)
   std::map<int, ShmTable> shm;
+  std::set<spx_ctx*> deferred;  // contexts with reservations waiting for their adm_ev
   ~ChainAdmission();
 };
 ChainAdmission& adm() {
@@ -691,6 +695,8 @@ int adm_budget_locked(ChainAdmission& a, const spx_ctx* ctx) {
   return ctx->n_cu;
 }
 
+void adm_settle_locked(ChainAdmission& a, spx_ctx* ctx, bool drained);
+
 // Decide the chain of the call starting now.  Returns true when the call holds
 // a reservation, which adm_release must return once the call's launches ran.
 bool adm_acquire(spx_ctx* ctx) {
@@ -702,6 +708,12 @@ bool adm_acquire(spx_ctx* ctx) {
   bool ok;
   {
     std::lock_guard<std::mutex> lk(a.mu);
+    // reservations whose launches have run (deferred by calls that did not
+    // wait for them), this context's and every other's in the process
+    for (auto it = a.deferred.begin(); it != a.deferred.end();) {
+      spx_ctx* d = *it++;  // (adm_settle_locked may erase d)
+      adm_settle_locked(a, d, false);
+    }
     const int cap = adm_budget_locked(a, ctx);
     int& used = a.used[ctx->device];
     const int extra = std::max(0, B - ctx->adm_blocks);  // 0: this context holds B already
@@ -728,9 +740,7 @@ bool adm_acquire(spx_ctx* ctx) {
   return ok;
 }
 
-void adm_release(spx_ctx* ctx) {
-  ChainAdmission& a = adm();
-  std::lock_guard<std::mutex> lk(a.mu);
+void adm_release_locked(ChainAdmission& a, spx_ctx* ctx) {
   if (ctx->adm_calls > 0 && --ctx->adm_calls == 0) {
     int& used = a.used[ctx->device];
     used -= ctx->adm_blocks;
@@ -739,10 +749,32 @@ void adm_release(spx_ctx* ctx) {
   }
 }
 
-void adm_release_cb(void* p) { adm_release(static_cast<spx_ctx*>(p)); }
+void adm_release(spx_ctx* ctx) {
+  ChainAdmission& a = adm();
+  std::lock_guard<std::mutex> lk(a.mu);
+  adm_release_locked(a, ctx);
+}
+
+// Release a context's deferred reservations once their launches have run:
+// `drained` (its stream was just synchronised) or its adm_ev has completed.
+void adm_settle_locked(ChainAdmission& a, spx_ctx* ctx, bool drained) {
+  if (ctx->adm_deferred == 0) return;
+  if (!drained && (!ctx->adm_ev || hipEventQuery(ctx->adm_ev) != hipSuccess)) return;
+  for (; ctx->adm_deferred > 0; --ctx->adm_deferred) adm_release_locked(a, ctx);
+  a.deferred.erase(ctx);
+}
+void adm_settle(spx_ctx* ctx, bool drained) {
+  ChainAdmission& a = adm();
+  std::lock_guard<std::mutex> lk(a.mu);
+  adm_settle_locked(a, ctx, drained);
+}
 
 // Holds a call's reservation: released at once when the call drained its
-// stream, else by a host callback behind the call's launches on the stream.
+// stream, else deferred behind an event recorded after the call's launches
+// and released by the first of: a drain of the context (spx_sync, a State
+// pull, spx_destroy), its next call, or any admission decision in the process
+// that finds the event complete.  (A host callback on the stream did the same
+// promptly, but cost every call ~46 us of stream time: tools/dbg/call_overhead.py.)
 struct AdmCall {
   spx_ctx* ctx;
   bool held = false;
@@ -750,8 +782,17 @@ struct AdmCall {
   explicit AdmCall(spx_ctx* c) : ctx(c) {}
   ~AdmCall() {
     if (!held) return;
-    if (drained || hipLaunchHostFunc(ctx->stream, adm_release_cb, ctx) != hipSuccess)
+    if (!drained && !ctx->adm_ev &&
+        hipEventCreateWithFlags(&ctx->adm_ev, hipEventDisableTiming) != hipSuccess)
+      ctx->adm_ev = nullptr;
+    if (drained || !ctx->adm_ev || hipEventRecord(ctx->adm_ev, ctx->stream) != hipSuccess) {
       adm_release(ctx);
+      return;
+    }
+    ChainAdmission& a = adm();
+    std::lock_guard<std::mutex> lk(a.mu);
+    ctx->adm_deferred++;
+    a.deferred.insert(ctx);
   }
 };
 
@@ -996,6 +1037,7 @@ int pull_state(spx_ctx* ctx) {
   HIPC(hipMemcpyAsync(ctx->h_st, ctx->st, sizeof(State), hipMemcpyDeviceToHost, ctx->stream));
   HIPC(hipStreamSynchronize(ctx->stream));
   ctx->st_fresh = true;
+  adm_settle(ctx, true);
   return SPX_OK;
 }
 
@@ -1600,7 +1642,14 @@ int spx_destroy(spx_ctx* ctx) {
   if (ctx->ev_done) (void)hipEventDestroy(ctx->ev_done);
   (void)hipSetDevice(ctx->device);
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
-  while (ctx->adm_calls > 0) adm_release(ctx);  // (callbacks ran at the sync; error paths)
+  {
+    ChainAdmission& a = adm();
+    std::lock_guard<std::mutex> lk(a.mu);
+    adm_settle_locked(a, ctx, true);
+    a.deferred.erase(ctx);
+    while (ctx->adm_calls > 0) adm_release_locked(a, ctx);  // (error paths)
+  }
+  if (ctx->adm_ev) (void)hipEventDestroy(ctx->adm_ev);
   free_buffers(ctx);
   for (auto* pool : {&ctx->ev, &ctx->evc})
     for (auto& e : *pool) {
@@ -2013,6 +2062,7 @@ int spx_set_window(spx_ctx* ctx, int K) {
 int spx_sync(spx_ctx* ctx) {
   if (!ctx) return SPX_E_ARG;
   HIPC(hipStreamSynchronize(ctx->stream));
+  adm_settle(ctx, true);
   return rp_recover(ctx);
 }
 
