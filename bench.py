@@ -83,6 +83,8 @@ def parse():
                          "timed region (0: every 8th elimination / flush; an event node costs "
                          "~6 us of stream time, and a timed window is launched directly: "
                          "~21 us per timed window at config 3)")
+    ap.add_argument("--dump-history", default="",
+                    help="diagnostic: rank 0 saves the run's pivot sequence (.npy) here")
     ap.add_argument("--cpu-seconds", type=float, default=15.0,
                     help="budget of the CPU-baseline sample (0 disables)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles",
@@ -457,6 +459,8 @@ def main():
         pass
 
     hist = eng.history() if rank == 0 else None
+    if hist is not None and args.dump_history:
+        np.save(args.dump_history, np.asarray(hist, dtype=np.int64))
     cpu = None
     if hist is not None and world == 1 and args.cpu_seconds > 0:
         cpu = cpu_baseline(m, n, args.seed, args.rule, args.cpu_seconds, hist.tolist())

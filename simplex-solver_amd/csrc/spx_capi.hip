@@ -143,6 +143,7 @@ struct spx_ctx {
   // persistent pivot chain of a window (spx_chain.hpp): record buffers and mode
   unsigned long long* gr_enter = nullptr;  // ENTER_REC x CHAIN_MAX_BLOCKS granules
   unsigned long long* gr_ratio = nullptr;  // RATIO_REC x CHAIN_MAX_BLOCKS granules
+  size_t A_bytes = 0, gr_bytes = 0;  // (spx_ctx::kept)
   int chain_mode = 0;      // 0: persistent chain when it fits, 1: launch per phase
   int chain_min_blocks = 0;
   // admission of the persistent chain (process-wide block budget per device):
@@ -161,6 +162,14 @@ struct spx_ctx {
   bool peer_ok = false;
   ChainPeers peers{};
   std::vector<void*> ipc_open;  // IPC-mapped peer buffers (closed on reload / destroy)
+  // Buffers this context exported to peers (spx_peer_export: the tableau and
+  // the record buffer) are not freed before spx_destroy: a reload keeps them
+  // here and reuses one only for a buffer of exactly its size, so a new
+  // allocation never lands at an address a peer has mapped before (an IPC
+  // mapping that a runtime hands back for a recycled address would read freed
+  // or foreign memory).
+  bool exported = false;
+  std::vector<std::pair<void*, size_t>> kept;
   ChainPeers* d_peers = nullptr;  // device copy of `peers` (the chain kernel's argument)
   int peer_same_dev = 1;        // ranks whose chains share this rank's GPU
   int peer_B = 0, peer_cb = BLK;  // the shard chain's grid, agreed by every rank at import
@@ -246,6 +255,13 @@ void close_peers(spx_ctx* ctx) {
 int free_buffers(spx_ctx* ctx) {
   drop_graphs(ctx);
   close_peers(ctx);
+  if (ctx->exported) {  // (see spx_ctx::kept)
+    if (ctx->A) ctx->kept.emplace_back(ctx->A, ctx->A_bytes);
+    if (ctx->gr_ratio) ctx->kept.emplace_back(ctx->gr_ratio, ctx->gr_bytes);
+    ctx->A = nullptr;
+    ctx->gr_ratio = nullptr;
+    ctx->exported = false;
+  }
   dfree(ctx->A);
   dfree(ctx->obj);
   dfree(ctx->F);
@@ -1191,6 +1207,17 @@ int rp_recover(spx_ctx* ctx) {
   }
 }
 
+// A kept (once exported) buffer of exactly `bytes`, if any (spx_ctx::kept).
+bool take_kept(spx_ctx* ctx, size_t bytes, void** out) {
+  for (auto it = ctx->kept.begin(); it != ctx->kept.end(); ++it)
+    if (it->second == bytes) {
+      *out = it->first;
+      ctx->kept.erase(it);
+      return true;
+    }
+  return false;
+}
+
 int alloc_common(spx_ctx* ctx, int64_t m_local, int64_t N, int64_t m_global, int64_t row0) {
   free_buffers(ctx);
   ctx->m_local = m_local;
@@ -1202,7 +1229,9 @@ int alloc_common(spx_ctx* ctx, int64_t m_local, int64_t N, int64_t m_global, int
   choose_geometry(ctx);
   ctx->hist_cap = 1 << 20;
   HIPC(hipSetDevice(ctx->device));
-  HIPC(hipMalloc(&ctx->A, sizeof(double) * ctx->ld * N));
+  ctx->A_bytes = sizeof(double) * ctx->ld * N;
+  if (!take_kept(ctx, ctx->A_bytes, reinterpret_cast<void**>(&ctx->A)))
+    HIPC(hipMalloc(&ctx->A, ctx->A_bytes));
   HIPC(hipMalloc(&ctx->obj, sizeof(double) * N));
   HIPC(hipMalloc(&ctx->F, sizeof(double) * 2 * ctx->ld));
   HIPC(hipMalloc(&ctx->P, sizeof(double) * N));
@@ -1245,7 +1274,10 @@ int alloc_common(spx_ctx* ctx, int64_t m_local, int64_t N, int64_t m_global, int
                       (ctx->sharded ? (size_t)(HS_PLANE_SHARD + 2) * CHAIN_SH_SLOTS
                                     : (size_t)(HS_PLANE_1GPU + 2) * CHAIN_MAX_BLOCKS);
     HIPC(hipMalloc(&ctx->gr_enter, ge));
-    if (ctx->sharded && !ctx->loop) {
+    ctx->gr_bytes = gq;
+    if (take_kept(ctx, gq, reinterpret_cast<void**>(&ctx->gr_ratio))) {
+      // (a kept record buffer: allocated as below by an earlier load)
+    } else if (ctx->sharded && !ctx->loop) {
       if (hipExtMallocWithFlags((void**)&ctx->gr_ratio, gq, hipDeviceMallocUncached) != hipSuccess) {
         (void)hipGetLastError();
         HIPC(hipMalloc(&ctx->gr_ratio, gq));
@@ -1508,6 +1540,7 @@ int spx_peer_export(spx_ctx* ctx, void* out, int64_t cap) {
   HIPC(hipSetDevice(ctx->device));
   HIPC(hipIpcGetMemHandle(&b.hA, ctx->A));
   HIPC(hipIpcGetMemHandle(&b.hR, ctx->gr_ratio));
+  ctx->exported = true;
   b.ld = ctx->ld;
   b.row0 = ctx->row0;
   b.m_local = ctx->m_local;
@@ -1650,7 +1683,10 @@ int spx_destroy(spx_ctx* ctx) {
     while (ctx->adm_calls > 0) adm_release_locked(a, ctx);  // (error paths)
   }
   if (ctx->adm_ev) (void)hipEventDestroy(ctx->adm_ev);
+  ctx->exported = false;  // (destroy: the exported buffers go too)
   free_buffers(ctx);
+  for (auto& k : ctx->kept) (void)hipFree(k.first);
+  ctx->kept.clear();
   for (auto* pool : {&ctx->ev, &ctx->evc})
     for (auto& e : *pool) {
       (void)hipEventDestroy(e.first);
