@@ -276,6 +276,11 @@ def _free_port():
 @pytest.mark.parametrize("args", [
     ["--rows", "600", "--cols", "900", "--window", "8"],
     ["--rows", "400", "--cols", "15984", "--window", "24", "--pivots", "100"],
+    # one context reloaded with LPs of other sizes and then the first again:
+    # the peers re-import buffers that were freed and allocated anew
+    # (the same-device flake)
+    ["--rows", "512", "--cols", "2048", "--window", "24", "--pivots", "101",
+     "--then", "1024x8000,512x2048,1024x8000"],
 ])
 def test_peer_chain_two_processes_ipc(args):
     """Two processes on GPU 0, no RCCL: IPC handles of each rank's tableau and
