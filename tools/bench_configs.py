@@ -30,7 +30,16 @@ import numpy as np  # noqa: E402
 
 from oracle import c_oracle as C  # noqa: E402
 from simplex_amd import synth  # noqa: E402
-from simplex_amd.engine import DeviceTableau  # noqa: E402
+from simplex_amd.engine import DeviceTableau as _DeviceTableau  # noqa: E402
+
+PAD = int(os.environ.get("SPX_LD_PAD", "-1"))  # column padding override (A/B runs)
+
+
+def DeviceTableau(dev):
+    e = _DeviceTableau(dev)
+    if PAD >= 0:
+        e.set_ld_pad(PAD)
+    return e
 
 
 def config2(window=0):
@@ -82,6 +91,7 @@ def config5(window=0, k=2048, k_cpu=60):
     stc, hc = C.solve(Tc, bc, rule="bland", max_iters=k_cpu)
     cpu_s = time.perf_counter() - t0
     return {"config": "5: degenerate 4096x4096 LP, Bland", "window": window, "gpu_pivots": k,
+            "ld_pad": PAD,
             "gpu_pivots_per_s": k / gpu_s, "status_after": st, "iters": it,
             "cpu_oracle_pivots_per_s": len(hc) / cpu_s, "cpu_threads": C.threads(),
             "first_pivots_match_oracle": [tuple(x) for x in hist[:len(hc)]] == hc}
@@ -102,7 +112,7 @@ def full_solve(name, window=24):
         gpu_s = time.perf_counter() - t0
     return {"config": f"{name}: {fx['m']}x{fx['n']} {fx['kind']} LP, {fx['rule']}, "
                       + (f"first {cap} pivots" if cap else "solve to optimality"),
-            "window": window, "gpu_s": gpu_s, "pivots": res.iters,
+            "window": window, "ld_pad": PAD, "gpu_s": gpu_s, "pivots": res.iters,
             "gpu_pivots_per_s": res.iters / gpu_s, "status": res.status,
             "objective": res.objective, "matches_fixture": res.iters == fx["pivots"]
             and res.objective == fx["objective"],
@@ -115,6 +125,9 @@ def full_solve(name, window=24):
 
 
 if __name__ == "__main__":
+    if "--config5-k24" in sys.argv:
+        print(json.dumps(config5(24, k=8192)), flush=True)
+        sys.exit(0)
     if "--full" in sys.argv:
         for name in ("config3", "config5"):
             print(json.dumps(full_solve(name)), flush=True)
