@@ -232,7 +232,7 @@ def test_window_timed_graph_and_chunks(eng_cls, K):
     assert [tuple(x) for x in outs[0][0]] == hist and np.array_equal(outs[0][1], ref)
 
 
-@pytest.mark.parametrize("pad", [0, 2, 130])
+@pytest.mark.parametrize("pad", [0, 2, 130, 1024])
 def test_window_ld_padding_and_odd_rows(eng_cls, pad):
     from simplex_amd import synth
     T, basis = synth.full_tableau("dense", 257, 300, 4)
