@@ -65,10 +65,9 @@ def parse():
                     help="windowed elimination: K pivots per tableau pass (0 = off, "
                          "-1 = default: %d, on one GPU and on row shards)" % DEFAULT_WINDOW)
     ap.add_argument("--chain", type=int, default=0,
-                    help="window pivot chain: 0 one persistent launch per window (default, "
-                         "single GPU), 1 two launches per pivot, 2 / 3 persistent with 256- / "
-                         "512-thread blocks, 4 / 5 persistent on one XCD (512-thread / "
-                         "two 256-thread blocks per CU)")
+                    help="window pivot chain: 0 one persistent launch per window (default), "
+                         "1 two launches per pivot, 2 / 3 persistent with 256- / 512-thread "
+                         "blocks (at N > 1: the row-sharded chain's block width)")
     ap.add_argument("--chain-blocks", type=int, default=0, help="persistent chain grid (0: minimum)")
     ap.add_argument("--peer", type=int, default=1,
                     help="N > 1 windows: 1 the row-sharded persistent chain (peer records over "
@@ -407,8 +406,7 @@ def main():
         c_ms, c_n = eng.chain_timing(reset=True)
         eng.set_chain_timing(False)
         nb = eng.chain_blocks()
-        chain = {"kernel": ("spx::chain_shard_kernel" if world > 1 else
-                            "spx::chain_xcd_kernel" if args.chain >= 4 else "spx::chain_kernel")
+        chain = {"kernel": ("spx::chain_shard_kernel" if world > 1 else "spx::chain_kernel")
                  if nb else "spx::lazy_ratio_kernel + spx::lazy_norm_kernel",
                  "bound": "latency: two in-launch all-to-all exchanges and two dependent "
                           "HBM gathers per pivot (DESIGN.md 4b)",

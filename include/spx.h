@@ -227,9 +227,8 @@ int spx_chain_timing(spx_ctx* ctx, double* total_ms, int64_t* count, int reset);
  * (default) runs them as ONE persistent launch when the tableau fits (at most
  * 512 x CUs columns and rows, single-GPU contexts), mode 1 as two
  * launches per pivot, modes 2 / 3 force the persistent chain's 256- / 512-thread
- * blocks, modes 4 / 5 run the persistent chain on ONE XCD (one 512-thread /
- * two 256-thread blocks per CU; K <= 24 and a tableau that fits 32 CUs, else
- * the spread chain).  Results are bit-identical.  min_blocks (0..256) raises the
+ * blocks; any other mode is SPX_E_ARG (round 4's one-XCD modes 4 / 5 were
+ * removed).  Results are bit-identical.  min_blocks (0..256) raises the
  * persistent grid above its minimum (tuning; 0 = minimum). */
 int spx_set_chain(spx_ctx* ctx, int mode, int min_blocks);
 /* Blocks of the persistent chain the loaded tableau uses (0: not used). */

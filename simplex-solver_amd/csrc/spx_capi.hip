@@ -146,6 +146,7 @@ struct spx_ctx {
   size_t A_bytes = 0, gr_bytes = 0;  // (spx_ctx::kept)
   int chain_mode = 0;      // 0: persistent chain when it fits, 1: launch per phase
   int chain_min_blocks = 0;
+  int chain_lean = 0;      // chain_kernel<.., LEAN>: no per-slot guards (SPX_CHAIN_LEAN, A/B hook)
   // admission of the persistent chain (process-wide block budget per device):
   // blocks this context holds, calls holding them (released by a stream host
   // callback once the call's launches have run), and whether the current call
@@ -282,9 +283,6 @@ int free_buffers(spx_ctx* ctx) {
   dfree(ctx->win.epoch);
   dfree(ctx->win.nlist);
   dfree(ctx->win.rec);
-  dfree(ctx->win.xcnt);
-  dfree(ctx->win.colrow);
-  dfree(ctx->win.inexact);
   dfree(ctx->gr_enter);
   dfree(ctx->gr_ratio);
   ctx->loaded = false;
@@ -489,30 +487,13 @@ int64_t chain_need(int64_t N, int64_t rows, int cb, int min_blocks) {
 // refused admission, or a tableau wider than CB x CUs columns).  Row shards
 // take the geometry every rank agreed on at spx_peer_import /
 // spx_peer_chain_local (shard_geometry), so no rank decides alone.
-// The one-XCD chain (chain_xcd_kernel): mode 4, B blocks of 512 threads on one
-// XCD (one per CU), each owning <= 512 columns and <= 256 rows; mode 5, B
-// blocks of 256 threads (two per CU), <= 256 columns and <= 128 rows.  The
-// window histories live in LDS (K <= 24).  Returns B, or 0 when the tableau or
-// the window does not fit one XCD.
-int chain_xcd_blocks(const spx_ctx* ctx, int cb) {
-  if (ctx->sharded || ctx->win_k > 24) return 0;
-  const int per_xcd = std::max(1, ctx->n_cu / 8) * (cb == 256 ? 2 : 1);
-  const int64_t need = std::max<int64_t>({(ctx->N - 1 + cb - 1) / cb,
-                                          (ctx->m_local + cb / 2 - 1) / (cb / 2), 1,
-                                          (int64_t)ctx->chain_min_blocks});
-  return need <= per_xcd && need <= 64 ? (int)need : 0;
-}
-
 // Persistent chain geometry: B blocks of CB threads (one per CU, all
 // resident), each owning <= CB columns and <= CB rows.  Returns B (and CB in
-// *cb, whether it is the one-XCD chain in *xcd), or 0 when the chain does not
-// apply (the launch-per-phase mode, a refused admission, or a tableau wider
-// than CB x CUs columns).  Row shards take the geometry every rank agreed on
-// at spx_peer_import / spx_peer_chain_local (shard_geometry), so no rank
-// decides alone.
-int chain_blocks(spx_ctx* ctx, int* cb_out = nullptr, bool ignore_admission = false,
-                 bool* xcd_out = nullptr) {
-  if (xcd_out) *xcd_out = false;
+// *cb), or 0 when the chain does not apply (the launch-per-phase mode, a
+// refused admission, or a tableau wider than CB x CUs columns).  Row shards
+// take the geometry every rank agreed on at spx_peer_import /
+// spx_peer_chain_local (shard_geometry), so no rank decides alone.
+int chain_blocks(spx_ctx* ctx, int* cb_out = nullptr, bool ignore_admission = false) {
   if (ctx->chain_mode == 1) return 0;
   if (ctx->sharded) {  // shards: only once the peers are known
     if (!ctx->peer_ok) return 0;
@@ -521,15 +502,6 @@ int chain_blocks(spx_ctx* ctx, int* cb_out = nullptr, bool ignore_admission = fa
   }
   if (ctx->chain_denied && !ignore_admission) return 0;
   if (!ctx->n_cu) ctx->n_cu = device_cus(ctx->device);
-  if (ctx->chain_mode >= 4) {  // the one-XCD chain where it fits, else the spread one
-    const int xcb = ctx->chain_mode == 5 ? 256 : 512;
-    const int bx = chain_xcd_blocks(ctx, xcb);
-    if (bx > 0) {
-      if (cb_out) *cb_out = xcb;
-      if (xcd_out) *xcd_out = true;
-      return bx;
-    }
-  }
   const int cb = chain_cb(ctx->chain_mode, std::max<int64_t>(ctx->N, ctx->m_local), ctx->n_cu);
   if (cb_out) *cb_out = cb;
   const int64_t need = chain_need(ctx->N, ctx->m_local, cb, ctx->chain_min_blocks);
@@ -829,33 +801,21 @@ template <int KMAX>
 int enqueue_window_t(spx_ctx* ctx, int npiv, bool time_flush) {
   const int nbw = lazy_ratio_grid(ctx);
   int cb = BLK;
-  bool xcd = false;
-  const int B = chain_blocks(ctx, &cb, false, &xcd);
+  const int B = chain_blocks(ctx, &cb);
   std::pair<hipEvent_t, hipEvent_t>* ec = nullptr;
   if (ctx->time_chain) {
     int rc = next_event_pair(ctx, ctx->evc, ctx->evc_used, &ec);
     if (!rc) rc = record_event(ctx, ec->first);
     if (rc) return rc;
   }
-  if (B > 0 && xcd) {
-    // one 512-thread block per CU (mode 5: two 256-thread blocks); the first
-    // XCD to gather B of them runs the chain
-    const int cpb = (int)((ctx->N - 1 + B - 1) / B);
-    const int rpb = (int)std::max<int64_t>(1, (ctx->m_local + B - 1) / B);
-    if constexpr (KMAX <= 24) {
-      hipLaunchKernelGGL((cb == 256 ? chain_xcd_kernel<KMAX, 256> : chain_xcd_kernel<KMAX, 512>),
-                         dim3(cb == 256 ? 2 * ctx->n_cu : ctx->n_cu), dim3(cb), 0, ctx->stream,
-                         ctx->enter_part, ctx->st, (const Params*)ctx->prm,
-                         std::max(NWAVE * ctx->nbn, B), (const double*)ctx->A, ctx->ld,
-                         ctx->m_local, ctx->N, ctx->obj, ctx->win, npiv, ctx->basis, ctx->hist,
-                         ctx->gr_enter, ctx->gr_ratio, cpb, rpb, B);
-    }
-  } else if (B > 0) {
+  if (B > 0) {
     const int cpb = (int)((ctx->N - 1 + B - 1) / B);  // (B * cpb == N-1: xown owns the RHS)
     const int rpb = (int)std::max<int64_t>(1, (ctx->m_local + B - 1) / B);
     auto kern = ctx->sharded ? (cb == 512 ? chain_shard_kernel<KMAX, 512>
                                           : chain_shard_kernel<KMAX, 256>)
                              : (cb == 512 ? chain_kernel<KMAX, 512> : chain_kernel<KMAX, 256>);
+    if constexpr (KMAX % 4 == 0)
+      if (!ctx->sharded && cb == 256 && ctx->chain_lean) kern = chain_kernel<KMAX, 256, true>;
     hipLaunchKernelGGL(kern, dim3(B), dim3(cb), 0, ctx->stream, ctx->enter_part, ctx->st,
                        (const Params*)ctx->prm, std::max(NWAVE * ctx->nbn, B),
                        (const double*)ctx->A, ctx->ld, ctx->m_local, ctx->N, ctx->obj, ctx->win,
@@ -931,12 +891,7 @@ int enqueue_window_t(spx_ctx* ctx, int npiv, bool time_flush) {
   // a tail inside the flush measured 226 vs 182 us
   // (profiles/r03/ab_flush_tail_vs_rowfix.jsonl)
   hipLaunchKernelGGL(row_fix_kernel<KMAX>, dim3(ctx->nbn), dim3(BLK), 0, ctx->stream, ctx->A,
-                       ctx->ld, ctx->m_local, ctx->row0, ctx->N, ctx->win, npiv,
-                       (const State*)ctx->st, (const int64_t*)ctx->basis,
-                       // (the basic-column stamps only feed the one-XCD chain's row
-                       // gather: the spread chain measured slower with them,
-                       // profiles/r04/ab_basic_column_skip.jsonl)
-                       (xcd || ctx->chain_mode >= 4) ? ctx->m_local : (int64_t)0);
+                       ctx->ld, ctx->m_local, ctx->row0, ctx->N, ctx->win, npiv);
   HIPC(hipGetLastError());
   return SPX_OK;
 }
@@ -1250,12 +1205,6 @@ int alloc_common(spx_ctx* ctx, int64_t m_local, int64_t N, int64_t m_global, int
     HIPC(hipMalloc(&ctx->win.epoch, sizeof(uint32_t)));
     HIPC(hipMalloc(&ctx->win.nlist, sizeof(int32_t)));
     HIPC(hipMalloc(&ctx->win.rec, sizeof(double) * RECW * N));
-    HIPC(hipMalloc(&ctx->win.xcnt, sizeof(uint32_t) * 9));
-    HIPC(hipMemsetAsync(ctx->win.xcnt, 0, sizeof(uint32_t) * 9, ctx->stream));
-    HIPC(hipMalloc(&ctx->win.colrow, sizeof(uint64_t) * N));
-    HIPC(hipMemsetAsync(ctx->win.colrow, 0, sizeof(uint64_t) * N, ctx->stream));
-    HIPC(hipMalloc(&ctx->win.inexact, N));
-    HIPC(hipMemsetAsync(ctx->win.inexact, 0, N, ctx->stream));
     HIPC(hipMemsetAsync(ctx->win.nlist, 0, sizeof(int32_t), ctx->stream));
     HIPC(hipMemsetAsync(ctx->win.rec, 0, sizeof(double) * RECW * N, ctx->stream));
     HIPC(hipMemsetAsync(ctx->win.F, 0, sizeof(double) * KW * ctx->ld, ctx->stream));
@@ -1354,6 +1303,8 @@ int spx_create(spx_ctx** out, int device) {
   // tuning hook: SPX_FLUSH_TAIL=x (0..50) overrides the flush's tail share
   if (const char* ft = std::getenv("SPX_FLUSH_TAIL"))
     ctx->flush_tail = std::max(0, std::min(50, std::atoi(ft)));
+  // the single-GPU chain's LEAN slot chains (0 / 1; A/B hook, spx_chain.hpp)
+  if (const char* cl = std::getenv("SPX_CHAIN_LEAN")) ctx->chain_lean = std::atoi(cl) != 0;
   // windows per replayed graph (1..16; tuning hook)
   if (const char* gw = std::getenv("SPX_GRAPH_WINDOWS"))
     ctx->graph_windows = std::max(1, std::min(16, std::atoi(gw)));
@@ -1742,16 +1693,6 @@ int spx_load_rows(spx_ctx* ctx, const double* A, int64_t m_local, int64_t cols, 
   if (m_global > 0)
     HIPC(hipMemcpyAsync(ctx->basis, basis, sizeof(int64_t) * m_global, hipMemcpyHostToDevice,
                         ctx->stream));
-  if (!ctx->sharded && m_local > 0) {
-    // the basic columns' exactness, for the chain's row gather (colrow_of)
-    hipLaunchKernelGGL(basis_exact_kernel, dim3((unsigned)m_local), dim3(BLK), 0, ctx->stream,
-                       (const double*)ctx->A, ctx->ld, m_local, cols,
-                       (const int64_t*)ctx->basis, ctx->win);
-    hipLaunchKernelGGL(basis_stamp_kernel, dim3((unsigned)((m_local + BLK - 1) / BLK)), dim3(BLK),
-                       0, ctx->stream, (const int64_t*)ctx->basis, m_local, cols, (int64_t)0,
-                       ctx->win);
-    HIPC(hipGetLastError());
-  }
   HIPC(hipStreamSynchronize(ctx->stream));
   ctx->loaded = true;
   return SPX_OK;
@@ -2074,7 +2015,13 @@ int spx_probe_read(unsigned long long* out, int n) {
 }
 int spx_probe_read_chain(unsigned long long* out, int n) {
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(spx::spx_probe_chain),
-                             sizeof(unsigned long long) * std::min(n, 32 * 4 * 256)) == hipSuccess
+                             sizeof(unsigned long long) *
+                                 std::min(n, 32 * spx::PROBE_CHAIN_EV * 256)) == hipSuccess
+             ? 0 : -1;
+}
+int spx_probe_read_chain_hw(unsigned long long* out, int n) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(spx::spx_probe_chain_hw),
+                             sizeof(unsigned long long) * std::min(n, 256)) == hipSuccess
              ? 0 : -1;
 }
 // flush grid of the last window (diagnostic)
@@ -2243,11 +2190,13 @@ int spx_get_elim_variant(const spx_ctx* ctx, int64_t out[7]) {
 // tableau fits (<= 512 x CUs columns and rows; single-GPU contexts), 1 = two
 // launches per pivot (lazy_ratio -> lazy_norm), 2 / 3 = the persistent chain
 // with 256- / 512-thread blocks.  min_blocks raises the persistent grid above
-// its minimum (tuning; 0 = minimum).
+// its minimum (tuning; 0 = minimum).  (Round 4's one-XCD chains, modes 4 and
+// 5, measured slower than mode 0 on every A/B and were removed in round 5:
+// DESIGN.md §4b.)
 int spx_set_chain(spx_ctx* ctx, int mode, int min_blocks) {
   if (!ctx) return SPX_E_ARG;
-  CHECK_ARG(mode >= 0 && mode <= 5 && min_blocks >= 0 && min_blocks <= CHAIN_MAX_BLOCKS,
-            "chain mode must be 0..5, min_blocks 0..256");
+  CHECK_ARG(mode >= 0 && mode <= 3 && min_blocks >= 0 && min_blocks <= CHAIN_MAX_BLOCKS,
+            "chain mode must be 0..3 (modes 4 / 5 were removed), min_blocks 0..256");
   ctx->chain_mode = mode;
   ctx->chain_min_blocks = min_blocks;
   drop_graphs(ctx);

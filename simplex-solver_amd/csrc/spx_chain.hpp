@@ -45,22 +45,50 @@
 namespace spx {
 
 #ifdef SPX_PHASE_TIMING
-// per-block chain timestamps (tools/probe_phases.py --blocks): [q][event][block],
-// events 0 ratio record stored, 1 ratio poll done, 2 entering record stored,
-// 3 entering poll done (of slot q+1's ratio phase)
-__device__ unsigned long long spx_probe_chain[32 * 4 * 256];
-#define SPX_PROBE_CHAIN_R(role, q, ev)                                                    \
-  do {                                                                                   \
-    if (threadIdx.x == 0 && (role) < 256 && (q) < 32)                                    \
-      spx_probe_chain[((q) * 4 + (ev)) * 256 + (role)] = __builtin_amdgcn_s_memrealtime(); \
+// per-block chain timestamps (tools/probe_phases.py --blocks,
+// tools/probe_stragglers.py): [q][event][block], events 0 ratio record stored,
+// 1 ratio poll done, 2 entering record stored, 3 entering poll done (of slot
+// q+1's ratio phase), 4 / 5 the ratio / norm phase's dependent loads arrived,
+// 6 / 7 their pending slots applied; spx_probe_chain_hw[block] = HW_ID |
+// XCC_ID << 32 of the block's CU
+constexpr int PROBE_CHAIN_EV = 8;
+__device__ unsigned long long spx_probe_chain[32 * PROBE_CHAIN_EV * 256];
+__device__ unsigned long long spx_probe_chain_hw[256];
+#define SPX_PROBE_CHAIN_R(role, q, ev)                                                     \
+  do {                                                                                    \
+    if (threadIdx.x == 0 && (role) < 256 && (q) < 32)                                     \
+      spx_probe_chain[((q) * PROBE_CHAIN_EV + (ev)) * 256 + (role)] =                     \
+          __builtin_amdgcn_s_memrealtime();                                               \
   } while (0)
 #define SPX_PROBE_CHAIN(q, ev) SPX_PROBE_CHAIN_R(blockIdx.x, q, ev)
+// stamped by thread 0 once `cond` (a value of the awaited data) is known
+#define SPX_PROBE_CHAIN_T(q, ev, cond)                                                     \
+  do {                                                                                    \
+    if (threadIdx.x == 0 && blockIdx.x < 256 && (q) < 32 && (cond))                       \
+      spx_probe_chain[((q) * PROBE_CHAIN_EV + (ev)) * 256 + blockIdx.x] =                 \
+          __builtin_amdgcn_s_memrealtime();                                               \
+  } while (0)
+#define SPX_PROBE_CHAIN_HW()                                                               \
+  do {                                                                                    \
+    if (threadIdx.x == 0 && blockIdx.x < 256) {                                           \
+      unsigned hw_, xc_;                                                                  \
+      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw_));                   \
+      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xc_));                  \
+      spx_probe_chain_hw[blockIdx.x] = (unsigned long long)hw_ | ((unsigned long long)xc_ << 32); \
+    }                                                                                     \
+  } while (0)
 #else
 #define SPX_PROBE_CHAIN(q, ev) \
   do {                         \
   } while (0)
 #define SPX_PROBE_CHAIN_R(role, q, ev) \
   do {                                 \
+  } while (0)
+#define SPX_PROBE_CHAIN_T(q, ev, cond) \
+  do {                                 \
+  } while (0)
+#define SPX_PROBE_CHAIN_HW() \
+  do {                       \
   } while (0)
 #endif
 
@@ -626,7 +654,7 @@ __device__ __forceinline__ double sys_load(const double* p) {
 // written by the previous kernel (norm<INIT> or the previous window's chain);
 // the chain writes one partial per block there for the next window.
 // ---------------------------------------------------------------------------
-template <int KMAX, int CB>
+template <int KMAX, int CB, bool LEAN = false>
 __global__ __launch_bounds__(CB) void chain_kernel(
     Key* __restrict__ enter_part, State* st, const Params* __restrict__ prm, int n_ep,
     const double* __restrict__ A, int64_t ld, int64_t m, int64_t N, double* __restrict__ obj,
@@ -635,12 +663,18 @@ __global__ __launch_bounds__(CB) void chain_kernel(
     const ChainPeers* __restrict__ /*pe: shards only*/) {
   static_assert(KMAX <= 32, "slots are lane-indexed and fit the window buffers");
   constexpr int NW = CB / 64;
-  constexpr int CH = KMAX % 8 == 0 ? 8 : KMAX % 4 == 0 ? 4 : 2;
+  // LEAN (round 5): the slot chains carry no per-slot
+  // "s < q" select.  A slot s >= q is an exact identity instead: its f and p
+  // histories are +0 (LDS zeroed at the window start, record lanes >= q are
+  // +0), and v - (+0 * +0) = v for every v, -0 and NaN included.  Only a
+  // chunk of CH slots is guarded, by a uniform branch.
+  constexpr int CH = LEAN ? 4 : KMAX % 8 == 0 ? 8 : KMAX % 4 == 0 ? 4 : 2;
   // LH: the window histories f_s[i] (rows) and p_s[j] (columns) live in LDS,
   // slot-major, one column per thread: a phase reads its thread's slots once
   // and appends one, instead of a 2*KMAX-select register update on the path
   // to the record (and the winner's history is published straight from them)
   constexpr bool LH = KMAX * CB * 16 <= 128 * 1024;
+  static_assert(!LEAN || (LH && KMAX % 4 == 0), "LEAN needs the LDS histories");
   __shared__ double fsl[LH ? KMAX : 1][LH ? CB : 1];
   __shared__ double psl[LH ? KMAX : 1][LH ? CB : 1];
   __shared__ double hl33[NW];  // LH: the wave winners' RHS (the ratio record's extra)
@@ -713,6 +747,11 @@ __global__ __launch_bounds__(CB) void chain_kernel(
   // entered at slot s (j == c_s), p_s[j] == 0 under the skip rule
   uint32_t rmask = 0u, cmask = 0u, zmask = 0u;
   if (t == 0) lds_pin[b % PIN] = 0.0;
+  SPX_PROBE_CHAIN_HW();
+  if constexpr (LEAN) {  // slots s >= q read +0 histories (written at slot s only)
+#pragma unroll
+    for (int s = 0; s < KMAX; ++s) fsl[s][t] = psl[s][t] = 0.0;
+  }
   if (status0 != ST_RUNNING) {          // grid-uniform: no pivot in this window
     if (leader)
       for (int s = 0; s < npiv; ++s) win.made[s] = 0;  // (the flush counts made slots)
@@ -803,6 +842,7 @@ __global__ __launch_bounds__(CB) void chain_kernel(
                         st))
       return;
     SPX_PROBE(q, 2, 0, fv != 12345.678 && pcl != 12345.678);  // loads arrived
+    SPX_PROBE_CHAIN_T(q, 4, fv != 12345.678 && pcl != 12345.678);
     // RHS: apply slot q-1 (the slots before it are already in bcur)
     if (q > 0) bcur = apply_sel(bcur, i == r_prev, false, true, f_prev, prhs, skip);
     // apply_sel's special cases as masks: column c entered earlier in this
@@ -819,7 +859,8 @@ __global__ __launch_bounds__(CB) void chain_kernel(
             for (int u = 0; u < CH; ++u) {
               const int s = c8 + u;
               const double x = msub(fv, fs[s], rdlane(pcl, s));
-              fv = s < q ? x : fv;
+              if constexpr (LEAN) fv = x;  // (s >= q: +0 histories, an identity)
+              else fv = s < q ? x : fv;
             }
           }
         }
@@ -832,8 +873,9 @@ __global__ __launch_bounds__(CB) void chain_kernel(
               const int s = c8 + u;
               const double p_s = rdlane(pcl, s);
               double x = msub(fv, fs[s], p_s);
-              x = ((rmask >> s) & 1u) ? p_s : x;
-              fv = s < q ? x : fv;
+              x = ((rmask >> s) & 1u) ? p_s : x;  // (bit s >= q is never set)
+              if constexpr (LEAN) fv = x;
+              else fv = s < q ? x : fv;
             }
           }
         }
@@ -854,6 +896,7 @@ __global__ __launch_bounds__(CB) void chain_kernel(
       }
     }
     SPX_PROBE(q, 2, 1, fv != 12345.678);  // slots applied
+    SPX_PROBE_CHAIN_T(q, 6, fv != 12345.678);
     if constexpr (LH) {
       fsl[q][t] = fv;
     } else {
@@ -939,6 +982,7 @@ __global__ __launch_bounds__(CB) void chain_kernel(
                         frl, ex, st))
       return;
     SPX_PROBE(q, 3, 0, v != 12345.678 && frl != 12345.678);  // loads arrived
+    SPX_PROBE_CHAIN_T(q, 5, v != 12345.678 && frl != 12345.678);
     const double piv = rdlane(frl, q);
     prhs = ex[0] / piv;  // p_q[rhs]: lazy_norm's p = v / piv of the RHS column
     // Special cases as masks: row r left earlier in the window (uniform: the
@@ -946,6 +990,9 @@ __global__ __launch_bounds__(CB) void chain_kernel(
     // p_s[j] == 0 under the skip rule (zmask: the value is kept)
     const uint32_t qmn = (1u << q) - 1u;
     const bool zb = (zmask & qmn) != 0u;
+    // LEAN: lane q holds the pivot element, which slot q of a chunk must not
+    // see (piv * +0 may be -0); lanes > q are +0 already
+    const double frm = LEAN ? (lane < q ? frl : 0.0) : frl;
     if (__ballot(lane < q && slot_r == r) == 0ull) {
       if (__ballot(jlive && ((zmask | cmask) & qmn) != 0u) == 0ull) {
 #pragma unroll
@@ -954,8 +1001,9 @@ __global__ __launch_bounds__(CB) void chain_kernel(
 #pragma unroll
             for (int u = 0; u < CH; ++u) {
               const int s = c8 + u;
-              const double x = msub(v, rdlane(frl, s), ps[s]);
-              v = s < q ? x : v;
+              const double x = msub(v, rdlane(frm, s), ps[s]);
+              if constexpr (LEAN) v = x;  // (s >= q: +0 histories, an identity)
+              else v = s < q ? x : v;
             }
           }
         }
@@ -966,10 +1014,11 @@ __global__ __launch_bounds__(CB) void chain_kernel(
 #pragma unroll
             for (int u = 0; u < CH; ++u) {
               const int s = c8 + u;
-              double x = msub(v, rdlane(frl, s), ps[s]);
-              x = ((zmask >> s) & 1u) ? v : x;
+              double x = msub(v, rdlane(frm, s), ps[s]);
+              x = ((zmask >> s) & 1u) ? v : x;  // (bits s >= q are never set)
               x = ((cmask >> s) & 1u) ? 0.0 : x;
-              v = s < q ? x : v;
+              if constexpr (LEAN) v = x;
+              else v = s < q ? x : v;
             }
           }
         }
@@ -990,6 +1039,7 @@ __global__ __launch_bounds__(CB) void chain_kernel(
       }
     }
     SPX_PROBE(q, 3, 1, v != 12345.678);  // slots applied
+    SPX_PROBE_CHAIN_T(q, 7, v != 12345.678);
     KeyP ek = keyp_none();
     double pq = 0.0;  // p_q[j]
     if (jlive) {
@@ -1090,576 +1140,6 @@ __global__ __launch_bounds__(CB) void chain_kernel(
     }
 
     SPX_PROBE(q, 1, 3, true);
-  }
-  // ---- the window ends after slot q (q pivots made) ----
-  if (stop_status != ST_RUNNING && leader) {
-    st->status = stop_status;
-    if (stop_status == ST_OPTIMAL) st->c_next = -1;
-    for (int s = q; s < npiv; ++s) win.made[s] = 0;
-  }
-  if (jlive) {
-    obj[j] = o;
-    if (tg != tg0) win.tag[j] = tg;
-  }
-  if (xown) {
-    obj[N - 1] = ox;
-    if (tgx != tgx0) win.tag[N - 1] = tgx;
-  }
-  if (q == 0) return;  // no pivot made: nothing to compact (the flush sees nm == 0)
-  // compact the window's touched columns into records for the flush (as
-  // lazy_norm's last slot): wave ballot + LDS prefix + one atomic per block;
-  // the RHS column (xown) follows its wave's own columns
-  const bool mine = jlive && (tg & TAG_EPOCH) == W;
-  const bool minex = xown && (tgx & TAG_EPOCH) == W;
-  __shared__ int wcnt[NW];
-  __shared__ int base;
-  const uint64_t bal = __ballot(mine);
-  const uint64_t balx = __ballot(minex);
-  if (lane == 0) wcnt[w] = __popcll(bal) + __popcll(balx);
-  __syncthreads();
-  if (t == 0) {
-    int tot = 0;
-    for (int x = 0; x < NW; ++x) tot += wcnt[x];
-    base = tot ? (int)__hip_atomic_fetch_add((gu32*)win.nlist, (unsigned)tot, __ATOMIC_RELAXED,
-                                             __HIP_MEMORY_SCOPE_AGENT)
-               : 0;
-  }
-  __syncthreads();
-  int pos = base + __popcll(bal & ((1ull << lane) - 1ull));
-  for (int x = 0; x < w; ++x) pos += wcnt[x];
-  if (mine && pos < N) {
-    double* rc_ = win.rec + (int64_t)pos * RECW;
-    reinterpret_cast<int64_t*>(rc_)[0] = j | ((int64_t)(tg >> 30) << 32);
-#pragma unroll
-    for (int s = 0; s < KMAX; ++s)
-      if (s < q) rc_[2 + s] = LH ? psl[s][t] : ps[s];
-  }
-  if (minex) {
-    const int px = pos - __popcll(bal & ((1ull << lane) - 1ull)) + __popcll(bal);
-    if (px < N) {
-      double* rc_ = win.rec + (int64_t)px * RECW;
-      reinterpret_cast<int64_t*>(rc_)[0] = (N - 1) | ((int64_t)(tgx >> 30) << 32);
-#pragma unroll
-      for (int s = 0; s < KMAX; ++s)
-        if (s < q) rc_[2 + s] = pxl[s];
-    }
-  }
-}
-
-// ---------------------------------------------------------------------------
-// chain_xcd_kernel<KMAX>: chain_kernel on ONE XCD ("The chain
-// on one XCD").  The spread chain's blocks are dealt over all 8 XCDs, so both
-// exchanges of a pivot are cross-XCD round trips (write-through sc1 granules,
-// ~2.2 us each with 64 blocks).  Here the grid is one 512-thread block per CU
-// (its LDS keeps it alone there; mode 5: two 256-thread blocks per CU) and
-// only B <= 32 (64) blocks of ONE XCD run the
-// chain: every block reads HW_REG_XCC_ID and takes a ticket on its XCD's
-// counter; the first XCD to hand out B tickets is chosen by a compare-and-swap
-// (or, after st->hs_ticks without one, ABORT: the window reports ST_NOTRES and
-// nothing was stored), its first B blocks take roles 0..B-1, and every other
-// block exits at once.  The records and history granules then stay in that
-// XCD's L2: plain (workgroup-scope atomic) stores, polled with sc1 loads that
-// bypass the L1 -- tools/xcd_exchange_probe.hip: 0.76 us per exchange against
-// 2.18 spread, the two gathers of a pivot 0.65 us slower from 32 CUs.  The
-// participants are co-resident by construction (each took its ticket while
-// running).  Block role b owns columns [b*cpb, ...) (one per thread, cpb <=
-// CB) and rows [b*rpb, ...) (rpb <= CB/2, on the waves after wave 0); the
-// window histories live in LDS (psl: CB columns, fsl: CB/2 rows; KMAX <= 24
-// fits the 160 KiB once or twice).  The arithmetic is chain_kernel's, operation for operation, so the
-// results are the same bytes.  win.xcnt is zeroed by the window's row_fix.
-// ---------------------------------------------------------------------------
-template <int KMAX, int CB = 512>
-__global__ __launch_bounds__(CB) __attribute__((amdgpu_waves_per_eu(CB == 256 ? 2 : 1)))
-void chain_xcd_kernel(
-    Key* __restrict__ enter_part, State* st, const Params* __restrict__ prm, int n_ep,
-    const double* __restrict__ A, int64_t ld, int64_t m, int64_t N, double* __restrict__ obj,
-    Window win, int npiv, int64_t* __restrict__ basis, int64_t* __restrict__ hist,
-    unsigned long long* gr_enter_, unsigned long long* gr_ratio_, int cpb, int rpb,
-    int B) {
-  static_assert(KMAX <= 32, "slots are lane-indexed and fit the window buffers");
-  constexpr int NW = CB / 64;
-  constexpr int CH = KMAX % 8 == 0 ? 8 : KMAX % 4 == 0 ? 4 : 2;
-  // the window histories in LDS, slot-major: p_s[j] one column per thread,
-  // f_s[i] one row per thread of waves 1..4 (RMAX rows per block)
-  // CB = 512: one block per CU (32 per XCD); CB = 256 (mode 5): two blocks
-  // per CU, 64 per XCD -- the spread chain's 4-wave blocks (its barrier and
-  // publish costs) with the one-XCD exchange
-  constexpr int RMAX = CB / 2;
-  static_assert((CB == 512 && KMAX * (CB + RMAX) * 8 <= 150 * 1024) ||
-                    (CB == 256 && KMAX * (CB + RMAX) * 8 <= 76 * 1024),
-                "LDS: one 512-thread or two 256-thread blocks per CU");
-  constexpr bool LH = true;
-  __shared__ double fsl[KMAX][RMAX];
-  __shared__ double psl[KMAX][CB];
-  __shared__ double hl33[NW];  // the wave winners' RHS (the ratio record's extra)
-  __shared__ int64_t bc_idx;  // the winner handed from wave 0 to the block
-  __shared__ double bc_val;
-  __shared__ int bc_blk;
-  __shared__ KeyP sk[NW];       // the waves' best keys (payload b = wave index)
-  __shared__ double hl[LH ? 1 : NW][34];  // their winners' histories (+ [33]: the row's RHS)
-  gu64* gr_enter = (gu64*)gr_enter_;
-  gu64* gr_ratio = (gu64*)gr_ratio_;
-  const int t = threadIdx.x;
-  const int lane = t & 63;
-  const int w = t >> 6;
-  const bool w0 = t < 64;
-  // --- everything that does not depend on a pivot, in one batch ---
-  const int32_t status0 = st->status;
-  const int64_t forced_c = st->forced_c;
-  const int64_t forced_r = st->forced_r;
-  const int64_t it0 = st->iters;
-  const int64_t hist_cap = st->hist_cap;
-  const int64_t hs_bound = st->hs_ticks;
-  const uint32_t E = *win.epoch;
-  const int32_t rule = prm->rule;
-  const double eps_piv = prm->eps_piv;
-  const double eps_opt = prm->eps_opt;
-  const int64_t n_enter = prm->n_enter;
-  const int64_t iter_limit = prm->iter_limit;
-  const bool skip = prm->skip_zero != 0;
-  const uint32_t W = (E + 1u) & TAG_EPOCH;  // this window's epoch
-  if (status0 != ST_RUNNING) {  // grid-uniform: no pivot in this window
-    if (blockIdx.x == 0 && t == 0)
-      for (int s = 0; s < npiv; ++s) win.made[s] = 0;  // (the flush counts made slots)
-    return;
-  }
-  // ---- the XCD and the roles: a ticket on my XCD's counter; the first XCD
-  // to hand out B tickets is chosen (one CAS); the rest of the grid exits ----
-  int b;
-  {
-    __shared__ int role_s;
-    if (t == 0) {
-      unsigned xcc;
-      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-      xcc &= 7u;
-      gu32* xc = (gu32*)win.xcnt;
-      const unsigned tk =
-          __hip_atomic_fetch_add(xc + xcc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      // the B-th arrival on my XCD claims the chain (a negative bound: the
-      // forced-ABORT test hook, no claim)
-      if (tk == (unsigned)B - 1u && hs_bound >= 0) {
-        unsigned z = 0u;
-        __hip_atomic_compare_exchange_strong(xc + 8, &z, xcc + 1u, __ATOMIC_RELAXED,
-                                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-      unsigned v;
-      for (;;) {
-        v = __hip_atomic_load(xc + 8, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (v != 0u) break;
-        if (hs_bound < 0 || (int64_t)(__builtin_amdgcn_s_memrealtime() - t0) > hs_bound) {
-          unsigned z = 0u;  // no XCD gathered B blocks in time: ABORT (unless one just did)
-          v = __hip_atomic_compare_exchange_strong(xc + 8, &z, 15u, __ATOMIC_RELAXED,
-                                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                  ? 15u : z;
-          break;
-        }
-        __builtin_amdgcn_s_sleep(1);
-      }
-      role_s = (v == xcc + 1u && tk < (unsigned)B) ? (int)tk : (v == 15u ? -2 : -1);
-    }
-    __syncthreads();
-    b = role_s;
-    if (b < 0) {  // not a participant (nothing stored); block 0 reports an ABORT
-      if (b == -2 && blockIdx.x == 0 && t == 0) {
-        st->status = ST_NOTRES;
-        for (int s = 0; s < npiv; ++s) win.made[s] = 0;
-      }
-      return;
-    }
-  }
-  const bool leader = b == 0 && t == 0;
-  // my column and my row
-  const int64_t j = (int64_t)b * cpb + t;
-  const bool jlive = t < cpb && j < N;
-  const int64_t jc = jlive ? j : 0;
-  // rows sit on waves 1.. when they fit (roff = 64), so the polling wave 0
-  // issues no row-side stores (f_q) that its next poll's vmcnt wait would
-  // also have to drain; the pivot bookkeeping is stored by the last thread
-  const int roff = rpb <= CB - 64 ? 64 : 0;
-  const int64_t i = (int64_t)b * rpb + (t - roff);
-  const bool trok = (unsigned)(t - roff) < (unsigned)RMAX;  // my fsl column (row threads)
-  const int trc = trok ? t - roff : 0;
-  const bool ilive = t >= roff && t - roff < rpb && i < m;
-  const int64_t ic = ilive ? i : 0;
-  double o = obj[jc];
-  uint32_t tg = jlive ? win.tag[jc] : 0u;
-  // my column's row if it is basic at the window start (-1: load the row)
-  const int64_t crow = jlive ? colrow_of(win, jc, it0) : -1;
-  const uint32_t tg0 = tg;
-  // The RHS column N-1 is never an entering candidate and its pivot-row value
-  // is the ratio record's p_q[rhs] (the row owner's current RHS / pivot), so
-  // when the host sizes the grid by the N-1 candidate columns (B * cpb == N-1:
-  // 64 blocks at config 3, a single-pass poll) the last thread of the last
-  // block keeps it beside its own column: objective value, tag, p history.
-  const bool xown = (int64_t)B * cpb == N - 1 && b == B - 1 && t == CB - 1;
-  double ox = xown ? obj[N - 1] : 0.0;
-  uint32_t tgx = xown ? win.tag[N - 1] : 0u;
-  const uint32_t tgx0 = tgx;
-  uint32_t zmx = 0u;
-  __shared__ double pxl[KMAX];  // p_s[N-1] (xown only)
-  double bcur = A[(N - 1) * ld + ic];   // current RHS of my row (stale + applied slots)
-  int64_t bas = basis[ic];              // basis[i] (Bland's tie key)
-  double fs[KMAX], ps[KMAX];            // f_s[i], p_s[j] of this window
-#pragma unroll
-  for (int s = 0; s < KMAX; ++s) fs[s] = ps[s] = 0.0;
-  int64_t slot_r = 0, slot_c = -1;      // lane s: (r_s, c_s)
-  // per-thread slot masks (bit s): my row left at slot s (i == r_s), my column
-  // entered at slot s (j == c_s), p_s[j] == 0 under the skip rule
-  uint32_t rmask = 0u, cmask = 0u, zmask = 0u;
-  if (leader) {
-    // the flush's record counter; reset write-through and drained before this
-    // block's first record (every other block adds to it only after polling
-    // that record)
-    __hip_atomic_store((gu32*)win.nlist, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
-  int q = 0;
-  int64_t r_prev = -1;
-  double f_prev = 0.0, prhs = 0.0;  // my f_{q-1}[i]; p_{q-1}[rhs] = RHS of r_{q-1} / pivot
-  int32_t stop_status = ST_RUNNING;
-  for (; q < npiv; ++q) {
-    // ================= ratio phase q =================
-    SPX_PROBE_ROLE(b, q, 0, 0, true);
-    int64_t c;
-    double zc;
-    int wb = 0;
-    if (q == 0) {
-      // entering partials of the previous kernel (visible: kernel boundary)
-      Keys8 kk;
-      keys_issue(kk, enter_part, n_ep);
-      KeyR e = keys_reduce(kk, enter_part, n_ep);
-      wave_min_dpp(e);
-      c = e.row;
-      zc = c >= 0 ? obj[c] : 0.0;
-    } else {
-      if (w0) {
-        KeyP e;
-        const bool ok =
-            poll_records<false, 3>(gr_enter, B, rec_tag(W, q - 1, GK_ENTER), rule, e, st);
-        if (t == 0) {
-          bc_idx = ok ? e.row : -2;
-          bc_val = e.a;
-          bc_blk = (int)e.b;
-        }
-        SPX_PROBE_CHAIN_R(b, q - 1, 3);
-      }
-      __syncthreads();
-      c = bc_idx;
-      zc = bc_val;
-      wb = bc_blk;
-      if (c == -2) return;  // a wait timed out (ST_FAULT stored)
-    }
-    SPX_PROBE_ROLE(b, q, 0, 1, true);
-    if (forced_c >= 0) {
-      c = forced_c;
-      zc = obj[c];  // (forced pivots are single-pivot windows: q == 0)
-    }
-    const int64_t it = it0 + q;
-    if (c < 0) stop_status = ST_OPTIMAL;
-    else if (forced_r < 0 && it >= iter_limit) stop_status = ST_LIMIT;
-    if (stop_status != ST_RUNNING) break;  // grid-uniform
-    // column c on my row: stale + pending slots, in slot order; p_s[c] (lane
-    // s) from the winning entering record's history
-    double fv = A[c * ld + ic];
-    if constexpr (LH) {  // my row's f history, read while the gathers are in flight
-#pragma unroll
-      for (int s = 0; s < KMAX; ++s) fs[s] = fsl[s][trc];
-    }
-    double pcl = 0.0, unused[2];
-    if (q > 0 &&
-        !load_extras<0>(gr_enter, wb, ENTER_HDR, q, 0, rec_tag(W, q - 1, GK_ENTER), pcl, unused,
-                        st))
-      return;
-    SPX_PROBE_ROLE(b, q, 2, 0, fv != 12345.678 && pcl != 12345.678);  // loads arrived
-    // RHS: apply slot q-1 (the slots before it are already in bcur)
-    if (q > 0) bcur = apply_sel(bcur, i == r_prev, false, true, f_prev, prhs, skip);
-    // apply_sel's special cases as masks: column c entered earlier in this
-    // window or p_s[c] == 0 under the skip rule (uniform: the exact loop), my
-    // row left at slot s (rmask: p_s[c] replaces the msub on that lane).
-    // Otherwise a slot is one msub (~5 VALU ops instead of ~25).
-    const uint32_t qm = (1u << q) - 1u;
-    if (__ballot(lane < q && (slot_c == c || (skip && pcl == 0.0))) == 0ull) {
-      if (__ballot((rmask & qm) != 0u) == 0ull) {
-#pragma unroll
-        for (int c8 = 0; c8 < KMAX; c8 += CH) {
-          if (c8 < q) {
-#pragma unroll
-            for (int u = 0; u < CH; ++u) {
-              const int s = c8 + u;
-              const double x = msub(fv, fs[s], rdlane(pcl, s));
-              fv = s < q ? x : fv;
-            }
-          }
-        }
-      } else {
-#pragma unroll
-        for (int c8 = 0; c8 < KMAX; c8 += CH) {
-          if (c8 < q) {
-#pragma unroll
-            for (int u = 0; u < CH; ++u) {
-              const int s = c8 + u;
-              const double p_s = rdlane(pcl, s);
-              double x = msub(fv, fs[s], p_s);
-              x = ((rmask >> s) & 1u) ? p_s : x;
-              fv = s < q ? x : fv;
-            }
-          }
-        }
-      }
-    } else {
-#pragma unroll
-      for (int c8 = 0; c8 < KMAX; c8 += CH) {
-        if (c8 < q) {
-#pragma unroll
-          for (int u = 0; u < CH; ++u) {
-            const int s = c8 + u;
-            const bool act = s < q;
-            const bool isr = i == rdlane64(slot_r, s);
-            const bool isc = c == rdlane64(slot_c, s);
-            fv = apply_sel(fv, isr, isc, act, fs[s], rdlane(pcl, s), skip);
-          }
-        }
-      }
-    }
-    SPX_PROBE_ROLE(b, q, 2, 1, fv != 12345.678);  // slots applied
-    if constexpr (LH) {
-      if (trok) fsl[q][trc] = fv;
-    } else {
-#pragma unroll
-      for (int s = 0; s < KMAX; ++s) fs[s] = (s == q) ? fv : fs[s];
-    }
-    f_prev = fv;
-    KeyP k = keyp_none();
-    if (ilive) {
-      if (forced_r >= 0) {
-        if (i == forced_r) kmin2(k, 0.0, 0, i, 0.0, 0.0);
-      } else if (fv > eps_piv) {
-        const double rq = bcur / fv;
-        if (rq == rq) kmin2(k, rq, rule == RULE_BLAND ? bas : i, i, 0.0, 0.0);
-      }
-    }
-    SPX_PROBE_ROLE(b, q, 0, 2, fv != 12345.678);
-    // publish: the wave winner puts its f history and RHS in LDS, the block's
-    // winner is published by wave 0 (rows grow with the lane: Dantzig's tie key)
-    k = key_of_lane(k, wave_argmin(k.v, k.t, k.row >= 0, rule != RULE_BLAND));
-    if (ilive && k.row == i) {
-      if constexpr (LH) {
-        hl33[w] = bcur;
-      } else {
-#pragma unroll
-        for (int s = 0; s < KMAX; ++s)
-          if (s <= q) hl[w][s] = fs[s];
-        hl[w][33] = bcur;
-      }
-    }
-    if (lane == 0) sk[w] = KeyP{k.v, k.t, k.row, 0.0, (double)w};
-    SPX_PROBE_ROLE(b, q, 2, 2, k.v != 12345.678);  // wave argmin + LDS hand-off issued
-    __syncthreads();
-    SPX_PROBE_ROLE(b, q, 2, 3, true);              // every wave of the block arrived
-    if (w0) {
-      publish_local<NW, true, true>(gr_ratio, b, rec_tag(W, q, GK_RATIO), q + 1, sk,
-                               [&](int ww, int64_t row, int x) -> double {
-                                 if constexpr (LH)
-                                   return x == 33 ? hl33[ww]
-                                                  : fsl[x][(int)(row - (int64_t)b * rpb)];
-                                 else
-                                   return hl[ww][x];
-                               });
-      SPX_PROBE_CHAIN_R(b, q, 0);
-    }
-    // f_q for the flush / row_fix (later kernels): stored after the record, so
-    // these stores never queue in front of it
-    if (ilive) win.F[(int64_t)q * ld + i] = fv;
-    SPX_PROBE_ROLE(b, q, 0, 3, true);
-    // ================= norm phase q =================
-    SPX_PROBE_ROLE(b, q, 1, 0, true);
-    if (w0) {
-      KeyP rk;
-      const unsigned rtag = rec_tag(W, q, GK_RATIO);
-      const bool ok = rule == RULE_BLAND
-                          ? poll_records<true, 4>(gr_ratio, B, rtag, rule, rk, st)
-                          : poll_records<true, 3>(gr_ratio, B, rtag, rule, rk, st);
-      if (t == 0) {
-        bc_idx = ok ? rk.row : -2;
-        bc_blk = (int)rk.b;
-      }
-      SPX_PROBE_CHAIN_R(b, q, 1);
-    }
-    __syncthreads();
-    const int64_t r = bc_idx;
-    wb = bc_blk;
-    if (r == -2) return;
-    SPX_PROBE_ROLE(b, q, 1, 1, true);
-    if (q == 0 && leader) *win.epoch = W;  // every block has read E (its record carries W)
-    if (r < 0) {
-      stop_status = ST_UNBOUNDED;
-      break;
-    }
-    // row r on my column: stale + pending slots.  f_s[r] (lane s <= q, lane q
-    // the pivot element) and the row's RHS from the winning ratio record
-    // (a column basic at the window start is exactly e_crow there: no load)
-    double v = crow >= 0 ? (crow == r ? 1.0 : 0.0) : A[jc * ld + r];
-    if constexpr (LH) {  // my column's p history, read while the gathers are in flight
-#pragma unroll
-      for (int s = 0; s < KMAX; ++s) ps[s] = psl[s][t];
-    }
-    double frl = 0.0, ex[2];
-    if (!load_extras<1>(gr_ratio, wb, RATIO_HDR + 2, q + 1, RATIO_HDR, rec_tag(W, q, GK_RATIO),
-                        frl, ex, st))
-      return;
-    SPX_PROBE_ROLE(b, q, 3, 0, v != 12345.678 && frl != 12345.678);  // loads arrived
-    const double piv = rdlane(frl, q);
-    prhs = ex[0] / piv;  // p_q[rhs]: lazy_norm's p = v / piv of the RHS column
-    // Special cases as masks: row r left earlier in the window (uniform: the
-    // exact loop), my column entered at slot s (cmask: the value becomes 0),
-    // p_s[j] == 0 under the skip rule (zmask: the value is kept)
-    const uint32_t qmn = (1u << q) - 1u;
-    const bool zb = (zmask & qmn) != 0u;
-    if (__ballot(lane < q && slot_r == r) == 0ull) {
-      if (__ballot(jlive && ((zmask | cmask) & qmn) != 0u) == 0ull) {
-#pragma unroll
-        for (int c8 = 0; c8 < KMAX; c8 += CH) {
-          if (c8 < q) {
-#pragma unroll
-            for (int u = 0; u < CH; ++u) {
-              const int s = c8 + u;
-              const double x = msub(v, rdlane(frl, s), ps[s]);
-              v = s < q ? x : v;
-            }
-          }
-        }
-      } else {
-#pragma unroll
-        for (int c8 = 0; c8 < KMAX; c8 += CH) {
-          if (c8 < q) {
-#pragma unroll
-            for (int u = 0; u < CH; ++u) {
-              const int s = c8 + u;
-              double x = msub(v, rdlane(frl, s), ps[s]);
-              x = ((zmask >> s) & 1u) ? v : x;
-              x = ((cmask >> s) & 1u) ? 0.0 : x;
-              v = s < q ? x : v;
-            }
-          }
-        }
-      }
-    } else {
-#pragma unroll
-      for (int c8 = 0; c8 < KMAX; c8 += CH) {
-        if (c8 < q) {
-#pragma unroll
-          for (int u = 0; u < CH; ++u) {
-            const int s = c8 + u;
-            const bool act = s < q;
-            const bool isr = r == rdlane64(slot_r, s);
-            const bool isc = jc == rdlane64(slot_c, s);
-            v = apply_sel(v, isr, isc, act, rdlane(frl, s), ps[s], skip);
-          }
-        }
-      }
-    }
-    SPX_PROBE_ROLE(b, q, 3, 1, v != 12345.678);  // slots applied
-    KeyP ek = keyp_none();
-    double pq = 0.0;  // p_q[j]
-    if (jlive) {
-      const double p = v / piv;
-      pq = p;
-      zmask |= (skip && p == 0.0) ? (1u << q) : 0u;
-      cmask |= (j == c) ? (1u << q) : 0u;
-      if constexpr (!LH) {
-#pragma unroll
-        for (int s = 0; s < KMAX; ++s) ps[s] = (s == q) ? p : ps[s];
-      }
-      const bool nz = (p != 0.0) || !skip;
-      if (j == c) {
-        o = 0.0;
-      } else if (nz) {
-        o = msub(o, zc, p);
-      }
-      const bool tagged = (tg & TAG_EPOCH) == W;
-      if (nz) {
-        tg = W | ((j == c || (tagged && (tg & TAG_SPECIAL))) ? TAG_SPECIAL : 0u) |
-             (zb ? TAG_ZERO : 0u);
-      } else if (tagged) {
-        tg = tg | TAG_ZERO;
-      }
-      // key (o, j) under Dantzig, (0, j) under Bland; payload o (z_c)
-      if (j < n_enter && o < -eps_opt) kmin2(ek, rule == RULE_BLAND ? 0.0 : o, j, j, o, 0.0);
-    }
-    if (xown) {  // the RHS column: the same update with p = p_q[rhs] (never j == c)
-      const bool zbx = (zmx & qmn) != 0u;
-      zmx |= (skip && prhs == 0.0) ? (1u << q) : 0u;
-      const bool nz = (prhs != 0.0) || !skip;
-      if (nz) ox = msub(ox, zc, prhs);
-      const bool tagged = (tgx & TAG_EPOCH) == W;
-      if (nz) {
-        tgx = W | ((tagged && (tgx & TAG_SPECIAL)) ? TAG_SPECIAL : 0u) | (zbx ? TAG_ZERO : 0u);
-      } else if (tagged) {
-        tgx = tgx | TAG_ZERO;
-      }
-      pxl[q] = prhs;
-    }
-    if (ilive && i == r) bas = c;
-    rmask |= (i == r) ? (1u << q) : 0u;
-    if (lane == q) {
-      slot_r = r;
-      slot_c = c;
-    }
-    r_prev = r;
-    SPX_PROBE_ROLE(b, q, 1, 2, v != 12345.678);
-    ek = key_of_lane(ek, wave_argmin(ek.v, ek.t, ek.row >= 0, true));  // columns grow with the lane
-    if constexpr (LH) {
-      psl[q][t] = pq;
-    } else if (q + 1 < npiv && jlive && ek.row == j) {
-#pragma unroll
-      for (int s = 0; s < KMAX; ++s)
-        if (s <= q) hl[w][s] = ps[s];
-    }
-    if (lane == 0) sk[w] = KeyP{ek.v, ek.t, ek.row, ek.a, (double)w};
-    SPX_PROBE_ROLE(b, q, 3, 2, ek.v != 12345.678);  // wave argmin + LDS hand-off issued
-    __syncthreads();
-    SPX_PROBE_ROLE(b, q, 3, 3, true);               // every wave of the block arrived
-    if (w0) {
-      if (q + 1 < npiv) {
-        publish_local<NW, false, true>(gr_enter, b, rec_tag(W, q, GK_ENTER), q + 1, sk,
-                                  [&](int ww, int64_t col, int x) -> double {
-                                    if constexpr (LH)
-                                      return psl[x][(int)(col - (int64_t)b * cpb)];
-                                    else
-                                      return hl[ww][x];
-                                  });
-      } else if (t == 0) {
-        // the next window's pivot-0 partial (read after the kernel boundary)
-        KeyP kb = sk[0];
-#pragma unroll
-        for (int x = 1; x < NW; ++x) kmin2(kb, sk[x].v, sk[x].t, sk[x].row, sk[x].a, sk[x].b);
-        store_key(enter_part + b, KeyR{kb.v, kb.t, kb.row});
-        // the next window reduces n_ep partials (norm<INIT>'s per-WG count can
-        // exceed B, e.g. 512-thread blocks): the ones past this grid's must not
-        // keep an earlier kernel's keys
-        for (int x = b + B; x < n_ep; x += B) store_key(enter_part + x, keyr_none());
-      }
-      SPX_PROBE_CHAIN_R(b, q, 2);
-    }
-    // stores for later kernels, after the record (never queued in front of it):
-    // the pivot's bookkeeping (the flush and row_fix read p from the records)
-    if (b == 0 && t == CB - 1) {  // block 0's last thread: not in the polling wave
-      st->r = r;
-      st->c = c;
-      st->zc = zc;
-      st->piv = piv;
-      win.r[q] = r;
-      win.c[q] = c;
-      win.made[q] = 1;
-      basis[r] = c;
-      if (it < hist_cap) {
-        hist[2 * it] = r;
-        hist[2 * it + 1] = c;
-      }
-    }
-
-    SPX_PROBE_ROLE(b, q, 1, 3, true);
   }
   // ---- the window ends after slot q (q pivots made) ----
   if (stop_status != ST_RUNNING && leader) {

@@ -49,14 +49,6 @@ __device__ unsigned long long spx_probe_buf[1024 + 2 * 8192];
       spx_probe_buf[(((slot) * 4 + (kind)) * 4 + (phase)) & 1023] =                          \
           __builtin_amdgcn_s_memrealtime();                                                  \
   } while (0)
-// the same, stamped by the block with role `role` (the one-XCD chain's block 0
-// may not take part)
-#define SPX_PROBE_ROLE(role, slot, kind, phase, cond)                                       \
-  do {                                                                                       \
-    if ((role) == 0 && threadIdx.x == 0 && (cond))                                           \
-      spx_probe_buf[(((slot) * 4 + (kind)) * 4 + (phase)) & 1023] =                          \
-          __builtin_amdgcn_s_memrealtime();                                                  \
-  } while (0)
 // flush waves: [2*(4*b + w)] = exit time, [.. + 1] = HW_ID | XCC_ID << 32 | columns << 40
 __device__ unsigned long long spx_probe_wave[2 * 4 * 8192];
 #define SPX_PROBE_WAVE(w, cols)                                                              \
@@ -74,9 +66,6 @@ __device__ unsigned long long spx_probe_wave[2 * 4 * 8192];
 #else
 #define SPX_PROBE(slot, kind, phase, cond) \
   do {                                     \
-  } while (0)
-#define SPX_PROBE_ROLE(role, slot, kind, phase, cond) \
-  do {                                                \
   } while (0)
 #define SPX_PROBE_BLOCK(which) \
   do {                         \
@@ -104,26 +93,8 @@ struct Window {
   int32_t* nlist;    // 1             : records in `rec` (reset by lazy_ratio slot 0)
   double* rec;       // N x RECW      : the window's touched columns, compacted by the
                      //                 last lazy_norm: [j | path flags, pad, p_0 .. p_{K-1}]
-  uint32_t* xcnt;    // 9             : the one-XCD chain's per-XCD tickets + the chosen XCD
-                     //                 (spx_chain.hpp chain_xcd_kernel; zeroed by row_fix)
-  uint64_t* colrow;  // N             : (stamp << 32 | row) of the columns basic at the start of
-                     //                 the next window, stamped by row_fix with iters + 1
-  uint8_t* inexact;  // N             : 1 = basic at load but not an exact unit column
 };
 
-// Basic columns are exact unit vectors in the stored (stale) tableau: a column
-// enters as e_r (the flush writes it so) and, while it stays basic, every
-// pivot's p_s[j] is 0 (skipped) -- so row r of a column basic at the window
-// start is 1.0 at its own row and +0.0 elsewhere, which the chain's row gather
-// can synthesize instead of loading (one HBM page per column).  colrow[j]
-// holds that row, valid when its stamp equals the iteration count + 1 at the
-// window's start (any other path that pivots moves the count on).  Columns
-// basic at load are checked once (spx_load_rows: basis_exact_kernel); one that
-// is not exactly e_i is `inexact` until it enters.
-__device__ __forceinline__ int64_t colrow_of(const Window& win, int64_t j, int64_t it0) {
-  const uint64_t x = win.colrow[j];
-  return (uint32_t)(x >> 32) == (uint32_t)it0 + 1u ? (int64_t)(uint32_t)x : -1;
-}
 constexpr int RECW = KW + 2;  // doubles per record (272 B)
 
 // Apply pending pivot s to value v at (local row il, column j).
@@ -856,19 +827,13 @@ __global__ __launch_bounds__(BLK) void flush_lds_kernel(double* __restrict__ A, 
 template <int K>
 __global__ __launch_bounds__(BLK) void row_fix_kernel(double* __restrict__ A, int64_t ld,
                                                       int64_t m_local, int64_t row0, int64_t N,
-                                                      Window win, int npiv,
-                                                      const State* __restrict__ st,
-                                                      const int64_t* __restrict__ basis,
-                                                      int64_t m_basis) {
+                                                      Window win, int npiv) {
   (void)N;
   __shared__ double fr[K][K];  // fr[L][s] = f_s[r_L]
   __shared__ int64_t rows[K];
   __shared__ int lastL[K];
   // one thread per record of the window (the flush's compacted list: column,
   // path flags, p_0..p_{K-1}); all loads are independent: issue them together
-  // the next window's one-XCD chain starts from zeroed tickets (every launch of
-  // this window's chain -- its late blocks included -- has ended: stream order)
-  if (blockIdx.x == 0 && threadIdx.x < 9) win.xcnt[threadIdx.x] = 0u;
   const int kr = blockIdx.x * BLK + threadIdx.x;
   const bool live = kr < *win.nlist;
   const int64_t hdr = reinterpret_cast<const int64_t*>(win.rec)[(int64_t)(live ? kr : 0) * RECW];
@@ -894,15 +859,6 @@ __global__ __launch_bounds__(BLK) void row_fix_kernel(double* __restrict__ A, in
     lastL[threadIdx.x] = last;
   }
   __syncthreads();
-  // the next window's basic columns (single GPU: m_basis = m; shards: 0)
-  if (kr < m_basis) {
-    const int64_t j = basis[kr];
-    bool entered = false;  // entered in this window: an exact e_r now
-    for (int s = 0; s < madeK; ++s) entered |= win.c[s] == j;
-    if (j >= 0 && j < N - 1 && (entered || !win.inexact[j]))
-      win.colrow[j] = ((uint64_t)((uint32_t)st->iters + 1u) << 32) | (uint32_t)kr;
-  }
-  if (threadIdx.x < K && blockIdx.x == 0 && threadIdx.x < madeK) win.inexact[win.c[threadIdx.x]] = 0;
   if (madeK == 0 || !live || !fast) return;
 #pragma unroll
   for (int L = 0; L < K; ++L) {
@@ -915,34 +871,4 @@ __global__ __launch_bounds__(BLK) void row_fix_kernel(double* __restrict__ A, in
   }
 }
 
-}  // namespace spx
-
-namespace spx {
-// Load-time check of the basic columns (see colrow_of): block i tests column
-// basis[i] against e_i bit for bit (+0.0 and 1.0); a column that fails is
-// `inexact` (the chain then always loads it).  Two launches: flags, then the
-// stamps, so a column basic in two rows is never stamped.
-__global__ __launch_bounds__(BLK) void basis_exact_kernel(const double* __restrict__ A,
-                                                          int64_t ld, int64_t m, int64_t N,
-                                                          const int64_t* __restrict__ basis,
-                                                          Window win) {
-  const int64_t i = blockIdx.x;
-  const int64_t j = basis[i];
-  if (j < 0 || j >= N - 1) return;
-  bool bad = false;
-  for (int64_t k = threadIdx.x; k < m; k += BLK) {
-    const uint64_t x = (uint64_t)__double_as_longlong(A[j * ld + k]);
-    bad |= x != (k == i ? 0x3ff0000000000000ull : 0ull);
-  }
-  if (__syncthreads_or(bad) && threadIdx.x == 0) win.inexact[j] = 1;
-}
-__global__ __launch_bounds__(BLK) void basis_stamp_kernel(const int64_t* __restrict__ basis,
-                                                          int64_t m, int64_t N, int64_t iters,
-                                                          Window win) {
-  const int64_t i = (int64_t)blockIdx.x * BLK + threadIdx.x;
-  if (i >= m) return;
-  const int64_t j = basis[i];
-  if (j >= 0 && j < N - 1 && !win.inexact[j])
-    win.colrow[j] = ((uint64_t)((uint32_t)iters + 1u) << 32) | (uint32_t)i;
-}
 }  // namespace spx

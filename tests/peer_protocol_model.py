@@ -21,7 +21,16 @@ its hazards can be exercised on a CPU:
     peer may still gather one of them;
   * rank 0's time-limit stop bit riding in its ratio records;
   * the start handshake: arrival granules, a verdict fixed once per window by
-    compare-and-swap (GO / ABORT), the host's rerun of an aborted window.
+    compare-and-swap (GO / ABORT), the host's rerun of an aborted window;
+  * the poll's geometry: wave 0 of a block reads the nr * B record headers as
+    64 lanes x RPL records (RPL = 1, 2, 4, 8; clamped indices), which covers
+    every slot only while nr * B <= CHAIN_SH_SLOTS = 512 (config 4: 8 ranks x
+    64 blocks is exactly that);
+  * the owner-push row transport (round 5, `push=True`): the leaving row's
+    owner writes its stale values into every peer's inbox (tagged granules, two
+    halves by pivot parity) instead of every peer reading the owner's rows; the
+    window-end barrier is then not needed, since no peer reads another rank's
+    rows.
 
 The arithmetic is the spec's operation for operation: Python
 floats are IEEE doubles and `v - f * p` rounds the product, then the
@@ -60,13 +69,30 @@ def apply_sel(v, i_is_r, j_is_c, f, p, skip=True):
     return v - f * p
 
 
+CHAIN_SH_SLOTS = 512  # spx_chain.hpp: ratio record slots one poll covers
+
+
+def poll_slots(BR):
+    """The record slots wave 0 of a block reads in one poll pass
+    (spx_chain.hpp poll_records_n): lane l reads l, l + 64, ... (RPL records
+    per lane), clamped to BR - 1, so no lane branches around its loads."""
+    if BR > CHAIN_SH_SLOTS:
+        raise ValueError(f"{BR} ratio records exceed one poll ({CHAIN_SH_SLOTS})")
+    rpl = 1 if BR <= 64 else 2 if BR <= 128 else 4 if BR <= 256 else 8
+    return sorted({min(lane + 64 * x, BR - 1) for lane in range(64) for x in range(rpl)})
+
+
 class Device:
     """What every rank can reach: its peers' record buffers and stale rows."""
 
-    def __init__(self, nr, B, mutant=()):
-        self.nr, self.B, self.mutant = nr, B, set(mutant)
+    def __init__(self, nr, B, mutant=(), push=False):
+        self.nr, self.B, self.mutant, self.push = nr, B, set(mutant), push
         halves = 1 if "one_half" in self.mutant else 2
+        self.slots = poll_slots(nr * B)
+        assert self.slots == list(range(nr * B)), "the poll misses a record slot"
         self.ratio = [[dict() for _ in range(halves)] for _ in range(nr)]
+        # owner-push inboxes: [rank][parity half][column] -> (tag, stale value)
+        self.inbox = [[dict() for _ in range(2)] for _ in range(nr)]
         self.enter = [dict() for _ in range(nr)]
         self.done = [dict() for _ in range(nr)]
         self.arrive = {}
@@ -80,6 +106,10 @@ class Device:
 
 
 WAIT_LIMIT = 5.0  # s: the model's bound on every spin (the kernels' ~4 s)
+# Pause between polls.  0 yields the GIL at once; with hundreds of block
+# threads (config 4's 8 x 64) the spinning threads would starve the working
+# ones, so large worlds poll every POLL_SLEEP seconds instead.
+POLL_SLEEP = 0.0
 
 
 def _wait(pred, what, limit=None):
@@ -91,7 +121,7 @@ def _wait(pred, what, limit=None):
             return v
         if time.monotonic() - t0 > limit:
             raise Timeout(what)
-        time.sleep(0)
+        time.sleep(POLL_SLEEP)
 
 
 def _argmin(keys):
@@ -198,7 +228,7 @@ class Rank:
             if time.monotonic() - t0 > self.hs_bound:
                 want = ABORT
                 break
-            time.sleep(0)
+            time.sleep(POLL_SLEEP)
         with dev.cas:
             vw, vs = dev.verdict
             if vw > W:
@@ -267,9 +297,9 @@ class Rank:
             # ---- norm phase q: leaving row, p on my columns, entering key ----
             self.delay("poll_ratio", rank, b, q)
             tag = _tag(W, q, RATIO)
-            recs = _wait(lambda: ([dev.ratio[rank][h].get(x) for x in range(nr * B)]
+            recs = _wait(lambda: ([dev.ratio[rank][h].get(x) for x in dev.slots]
                                   if all(dev.ratio[rank][h].get(x, (None,))[0] == tag
-                                         for x in range(nr * B)) else None),
+                                         for x in dev.slots) else None),
                          f"rank {rank} block {b}: ratio records of slot {q}")
             if any(r[1][1] for r in recs):  # rank 0's stop request, seen by every rank here
                 with lock:
@@ -285,12 +315,29 @@ class Rank:
             owner = wslot // B
             piv = fr[q]
             prhs = rhs_r / piv
-            self.delay("gather_row", rank, b, q, owner)
-            src = dev.A[owner]  # the owner's stale rows (a peer pointer)
             rl = r - dev.row0[owner]
+            if dev.push and owner == rank:
+                # owner-push: my stale row values into every peer's inbox (the
+                # half of this pivot's parity), before my own slot work
+                for d in range(nr):
+                    if d != rank:
+                        for j in cols:
+                            dev.inbox[d][h][j] = (_tag(W, q, RATIO), self.A[rl, j])
+                        self.delay("between_peer_writes", rank, b, q)
+            self.delay("gather_row", rank, b, q, owner)
+            if dev.push and owner != rank:
+                tag_r = _tag(W, q, RATIO)
+                box = dev.inbox[rank][h]
+                row = _wait(lambda: ({j: box[j][1] for j in cols}
+                                     if all(box.get(j, (None,))[0] == tag_r for j in cols)
+                                     else None),
+                            f"rank {rank} block {b}: pushed row of slot {q}")
+            else:
+                src = dev.A[owner]  # the owner's stale rows (a peer pointer; my own rows)
+                row = {j: src[rl, j] for j in cols}
             ekey = None
             for j in cols:
-                v = src[rl, j]
+                v = row[j]
                 for s, (rs, cs, _) in enumerate(slots):
                     v = apply_sel(v, r == rs, j == cs, fr[s], ph[j][s])
                 p = v / piv
@@ -317,7 +364,8 @@ class Rank:
                     sh["prhs"].append(prhs)
                     sh["made"] = q + 1
         # ---- window end: no rank may flush while a peer still gathers its rows ----
-        if "no_done_barrier" not in dev.mutant:
+        # (owner-push: no peer reads my rows, so no barrier)
+        if "no_done_barrier" not in dev.mutant and not dev.push:
             for d in range(nr):
                 dev.done[d][rank * B + b] = _tag(W, 0, DONE)
             if b == 0:

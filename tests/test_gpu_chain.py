@@ -48,7 +48,7 @@ def _run(eng_cls, T, basis, K, mode, min_blocks=0, **kw):
 @pytest.mark.parametrize("K", [2, 8, 16, 24, 28, 32])
 @pytest.mark.parametrize("shape", [(2, 3), (17, 40), (300, 700), (1025, 2051)])
 @pytest.mark.parametrize("rule", ["dantzig", "bland"])
-@pytest.mark.parametrize("mode", [2, 3, 4, 5], ids=["cb256", "cb512", "xcd", "xcd256"])
+@pytest.mark.parametrize("mode", [2, 3], ids=["cb256", "cb512"])
 def test_chain_matches_lazy_chain_and_oracle(eng_cls, K, shape, rule, mode):
     T, basis = _random_tableau(*shape, seed=shape[0] * 7 + K)
     kw = dict(max_iters=3 * K + 5, rule=rule)
@@ -61,6 +61,30 @@ def test_chain_matches_lazy_chain_and_oracle(eng_cls, K, shape, rule, mode):
     st, hist = O.solve_tableau(ref, rb, rule=rule, max_iters=3 * K + 5)
     assert [tuple(x) for x in h] == hist and res.status == st
     assert np.array_equal(out, ref) and np.array_equal(b, rb)
+
+
+@pytest.mark.parametrize("K", [4, 8, 24, 28, 32])
+@pytest.mark.parametrize("shape", [(17, 40), (300, 700), (1025, 2051)])
+@pytest.mark.parametrize("rule", ["dantzig", "bland"])
+def test_chain_lean_variant_bit_exact(eng_cls, monkeypatch, K, shape, rule):
+    """The LEAN chain (SPX_CHAIN_LEAN=1, chain_kernel<.., true>: slot chains
+    without per-slot guards, slots past q run as exact identities on +0
+    histories) against the launch-per-phase chain and the oracle, with -0.0
+    entries and exact zeros (the skip rule's masked paths) in the tableau."""
+    T, basis = _random_tableau(*shape, seed=shape[0] * 13 + K, zero_frac=0.2)
+    m = shape[0] - 1
+    rng = np.random.default_rng(K)
+    neg = rng.random((m, T.shape[1] - 1 - m)) < 0.05
+    T[:m, :T.shape[1] - 1 - m][neg] = -0.0
+    kw = dict(max_iters=3 * K + 5, rule=rule)
+    res1, h1, out1, b1, _ = _run(eng_cls, T, basis, K, 1, **kw)
+    monkeypatch.setenv("SPX_CHAIN_LEAN", "1")
+    res, h, out, b, blocks = _run(eng_cls, T, basis, K, 2, **kw)
+    assert blocks >= 1
+    assert h == h1 and res.status == res1.status and out.tobytes() == out1.tobytes()
+    ref, rb = T.copy(), basis.copy()
+    st, hist = O.solve_tableau(ref, rb, rule=rule, max_iters=3 * K + 5)
+    assert [tuple(x) for x in h] == hist and np.array_equal(out, ref) and np.array_equal(b, rb)
 
 
 @pytest.mark.parametrize("K", [4, 8])
@@ -95,37 +119,19 @@ def test_chain_grid_sizes_bit_exact(eng_cls, min_blocks, mode):
     assert h == h1 and res.iters == res1.iters and out.tobytes() == out1.tobytes()
 
 
-@pytest.mark.parametrize("mode,min_blocks", [(4, 0), (4, 3), (4, 17), (4, 32),
-                                             (5, 0), (5, 3), (5, 33), (5, 64)])
-def test_chain_xcd_grid_sizes_bit_exact(eng_cls, mode, min_blocks):
-    """The one-XCD chain with more blocks than the minimum, up to a whole
-    XCD's 32 (mode 4: 512-thread blocks) or 64 (mode 5: two 256-thread blocks
-    per CU): the same bytes as the launch-per-phase chain and the oracle; past
-    that (or K > 24, or a tableau wider than one XCD's columns) the spread
-    chain runs."""
-    T, basis = _random_tableau(700, 2100, seed=21 + min_blocks)
-    res, h, out, b, blocks = _run(eng_cls, T, basis, 16, mode, min_blocks, max_iters=53)
-    res1, h1, out1, b1, _ = _run(eng_cls, T, basis, 16, 1, max_iters=53)
-    assert blocks == max(min_blocks, 5 if mode == 4 else 9)
-    assert h == h1 and res.iters == res1.iters and out.tobytes() == out1.tobytes()
-    ref, rb = T.copy(), basis.copy()
-    st, hist = O.solve_tableau(ref, rb, max_iters=53)
-    assert [tuple(x) for x in h] == hist and np.array_equal(out, ref)
-
-
-@pytest.mark.parametrize("mode", [4, 5])
-def test_chain_xcd_falls_back_to_spread(eng_cls, mode):
-    """Modes 4 / 5 where the one-XCD chain does not fit: K = 28 (its LDS
-    histories exceed 160 KiB) and a tableau wider than one XCD's columns run
-    the spread chain, same bytes."""
-    T, basis = _random_tableau(301, 20400, seed=6)
-    _, h, out, _, blocks = _run(eng_cls, T, basis, 24, mode, max_iters=30)
-    _, h1, out1, _, _ = _run(eng_cls, T, basis, 24, 1, max_iters=30)
-    assert blocks == 80 and h == h1 and out.tobytes() == out1.tobytes()
-    T, basis = _random_tableau(301, 2051, seed=7)
-    _, h, out, _, blocks = _run(eng_cls, T, basis, 28, mode, max_iters=60)
-    _, h1, out1, _, _ = _run(eng_cls, T, basis, 28, 1, max_iters=60)
-    assert blocks == 9 and h == h1 and out.tobytes() == out1.tobytes()
+def test_removed_chain_modes_rejected(eng_cls):
+    """Round 4's one-XCD chains (modes 4 / 5) were slower than mode 0 on every
+    same-box A/B and were removed in round 5: selecting one is
+    an argument error, and the context keeps its chain."""
+    from simplex_amd.engine import SpxError
+    T, basis = _random_tableau(17, 40, seed=3)
+    with eng_cls(0) as e:
+        e.set_window(8)
+        for mode in (4, 5, 6, -1):
+            with pytest.raises(SpxError):
+                e.set_chain(mode)
+        e.load(T, basis)
+        assert e.chain_blocks() >= 1
 
 
 @pytest.mark.parametrize("mode,nb", [(0, 80), (2, 80), (3, 40)])
@@ -140,7 +146,7 @@ def test_chain_wide_tableau_more_than_64_blocks(eng_cls, mode, nb):
 
 
 @pytest.mark.parametrize("K", [8, 24])
-@pytest.mark.parametrize("mode,nb", [(0, 64), (2, 64), (3, 32), (4, 32), (5, 64)])
+@pytest.mark.parametrize("mode,nb", [(0, 64), (2, 64), (3, 32)])
 def test_chain_config3_width_rhs_column_rides_along(eng_cls, K, mode, nb):
     """Config 3's width: N - 1 = 16384 candidate columns = 64 x 256, so the
     grid is 64 blocks (one record per polling lane) and the RHS column is kept
@@ -158,7 +164,7 @@ def test_chain_config3_width_rhs_column_rides_along(eng_cls, K, mode, nb):
 
 
 @pytest.mark.parametrize("K", [4, 24, 32])
-@pytest.mark.parametrize("mode", [0, 3, 4, 5])
+@pytest.mark.parametrize("mode", [0, 3])
 def test_chain_degenerate_bland_full_solve(eng_cls, K, mode):
     from simplex_amd import synth
     T, basis = synth.full_tableau("degenerate", 96, 96, seed=3)
@@ -292,7 +298,7 @@ def test_chain_budget_zero_runs_launch_per_phase(eng_cls):
         assert e.chain_stats()["persistent_calls"] == 1
 
 
-@pytest.mark.parametrize("mode", [0, 4, 5])
+@pytest.mark.parametrize("mode", [0, 3])
 def test_chain_handshake_forced_abort_reruns_bit_exact(eng_cls, mode):
     """spx_set_chain_handshake(ctx, -1): every persistent window aborts at its
     start handshake (ST_NOTRES) before any block stores anything; spx_solve,
@@ -553,13 +559,11 @@ def test_chain_timing_events(eng_cls, mode):
 
 
 @pytest.mark.parametrize("K", [8, 24])
-@pytest.mark.parametrize("mode", [0, 4, 5])
+@pytest.mark.parametrize("mode", [0, 3])
 def test_chain_basic_columns_not_unit_vectors_at_load(eng_cls, K, mode):
     """Basic columns that are not exact unit vectors at load (a tiny entry, a
-    -0.0, 1 + ulp) are ordinary data: the chain must not assume their values
-    (the one-XCD chain synthesizes the row gather of basic columns that ARE
-    exact; these are flagged at load).  Forced pivots on the affected rows
-    make each of them the leaving row."""
+    -0.0, 1 + ulp) are ordinary data: the chain must not assume their values.
+    Forced pivots on the affected rows make each of them the leaving row."""
     T, basis = _random_tableau(400, 1300, seed=40 + K)
     T[3, basis[7]] = 1e-300          # basic column of row 7 with an extra entry
     T[11, basis[2]] = -0.0           # -0.0 is not +0.0

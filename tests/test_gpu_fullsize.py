@@ -52,8 +52,6 @@ def _full_solve(name, window=24, chain=0):
         e.set_chain(chain)
         e.load_rows(Tf, obj, basis, fx["m"], 0)
         del Tf
-        if chain >= 4:
-            assert e.chain_blocks() == (32 if chain == 4 else 64)
         done = 0
         for k in sorted(int(x) for x in fx["checkpoint_sha256"]):
             r = e.solve(rule=fx["rule"], max_iters=k - done)
@@ -75,13 +73,13 @@ def _full_solve(name, window=24, chain=0):
     return fx
 
 
-@pytest.mark.parametrize("window,chain", [(24, 0), (28, 0), (24, 4), (24, 5)],
-                         ids=["k24", "k28", "k24-xcd512", "k24-xcd256"])
-def test_config3_dantzig_full_solve_pinned(window, chain):
+@pytest.mark.parametrize("window,chain,lean", [(24, 0, 0), (28, 0, 0), (24, 0, 1)],
+                         ids=["k24", "k28", "k24-lean"])
+def test_config3_dantzig_full_solve_pinned(window, chain, lean, monkeypatch):
     """Config 3 (8192 x 8192 dense LP, tableau 8193 x 16385): the whole
-    Dantzig solve at K = 24 and 28, and with the one-XCD chain forms (modes 4
-    and 5, whose row gather synthesizes the basic columns' values), vs the
-    oracle's, index for index."""
+    Dantzig solve at K = 24 and 28 (and with the LEAN chain, SPX_CHAIN_LEAN)
+    vs the oracle's, index for index."""
+    monkeypatch.setenv("SPX_CHAIN_LEAN", str(lean))
     _full_solve("config3", window=window, chain=chain)
 
 

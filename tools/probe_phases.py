@@ -89,9 +89,9 @@ def main():
                 print(f"       fine: keys reduced +{k0 - ph[0]:5.2f}  wave_min +{k1 - k0:5.2f}")
     if a.chain != 1:
         nb = e.chain_blocks()
-        cb = (ctypes.c_ulonglong * (32 * 4 * 256))()
-        assert lib.spx_probe_read_chain(cb, 32 * 4 * 256) == 0
-        ev = lambda q, k: [(cb[(q * 4 + k) * 256 + x] - t0) / 100.0 for x in range(nb)]
+        cb = (ctypes.c_ulonglong * (32 * 8 * 256))()
+        assert lib.spx_probe_read_chain(cb, 32 * 8 * 256) == 0
+        ev = lambda q, k: [(cb[(q * 8 + k) * 256 + x] - t0) / 100.0 for x in range(nb)]
         import statistics as S
         print(f"per-block exchange timing ({nb} blocks), us: publish spread = last - first "
               "record stored; seen = poll done - last record stored (min / median / max)")
