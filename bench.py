@@ -15,8 +15,16 @@ across the N GPUs (config 4): strong scaling, value = whole-job pivots/s.
 Output: ONE JSON line on rank 0 (contract in the task statement), with
 `roofline` for the elimination kernel (HIP-event timed inside the timed
 region; algorithmic bytes = 16 B per touched tableau element)
-and `cpu_baseline` (the numpy oracle on a bounded sample of the same
-workload, 1 thread, rank 0 at N=1 only).
+and `cpu_baseline` (rank 0 at N=1 only): the C/OpenMP restatement of the
+oracle (oracle/spx_oracle.c) on a bounded sample of the same workload with
+this job's CPU share (OMP_NUM_THREADS threads), beside the same C code on 1
+thread and the numpy oracle on 1 thread; every sample's pivots must equal the
+GPU's.
+
+At N > 1 the row-sharded persistent chain first passes a self-test on a small
+LP (both leaving-row transports, pull and owner-push, byte-identical to the
+reference path), then --peer-row auto times --row-trial windows of each on the
+bench's own tableau and every rank takes the faster (config.peer_chain).
 """
 from __future__ import annotations
 
@@ -73,6 +81,11 @@ def parse():
                     help="N > 1 windows: 1 the row-sharded persistent chain (peer records over "
                          "xGMI, after a bit-exact self-test against the RCCL path), 0 one RCCL "
                          "all-gather per pivot")
+    ap.add_argument("--peer-row", default="auto", choices=["auto", "pull", "push"],
+                    help="N > 1 peer chain: the leaving row's transport; auto times a few "
+                         "windows of each after the self-test and every rank takes the faster")
+    ap.add_argument("--row-trial", type=int, default=3,
+                    help="windows per transport in the --peer-row auto trial")
     ap.add_argument("--same-device", action="store_true",
                     help="N > 1 rehearsal on ONE GPU: every rank on GPU 0, peer-only shards "
                          "(no RCCL, IPC-mapped peers), the self-test against the single-GPU "
@@ -247,12 +260,14 @@ def _host_cpus():
             "affinity_cpus": aff, "OMP_NUM_THREADS": os.environ.get("OMP_NUM_THREADS")}
 
 
-def peer_selftest(eng, world, rank, K, tdist, torch, same_device=False):
+def peer_selftest(eng, world, rank, K, tdist, torch, same_device=False, chain=0):
     """Before the timed run: the row-sharded persistent chain must reproduce the
     RCCL launch-per-phase path byte for byte on a small LP (every rank, all
     ranks agree), else the bench falls back to RCCL.  --same-device (peer-only
     shards, no RCCL): the reference is the single-GPU windowed path on the
-    whole LP, and a failure ends the bench.  Returns (ok, note)."""
+    whole LP, and a failure ends the bench.  Both leaving-row transports run
+    (pull, then owner-push) and must give the same bytes.  Returns (ok, note,
+    push_ok)."""
     from simplex_amd import synth
     from simplex_amd.dist import row_partition
     from simplex_amd.engine import DeviceTableau, SpxError
@@ -266,19 +281,29 @@ def peer_selftest(eng, world, rank, K, tdist, torch, same_device=False):
     r0, r1 = row_partition(ms, world, rank)
     T, obj, basis = synth.tableau_rows("dense", ms, ns, 99, r0, r1, order="F")
     kw = dict(max_iters=4 * K + 5)
+
+    def run_peer(push):
+        eng.set_chain(chain)
+        eng.load_rows(T, obj, basis, ms, r0)
+        eng.enable_peer_chain(push=push)
+        if eng.chain_blocks() <= 0:
+            return None
+        eng.solve(**kw)
+        return eng.history().tobytes(), eng.tableau().tobytes()
+
     note = "ok"
     try:
-        eng.set_chain(0)
-        eng.load_rows(T, obj, basis, ms, r0)
-        eng.enable_peer_chain()
-        ok = eng.chain_blocks() > 0
-        if ok:
-            eng.solve(**kw)
-            a = (eng.history().tobytes(), eng.tableau().tobytes())
+        a = run_peer(False)
+        ok = a is not None
     except (SpxError, RuntimeError) as ex:
         ok, note = False, f"peer chain failed: {ex}"
     if not all_ok(ok):  # (every rank leaves here together: no collective is left pending)
-        return False, note if not ok else "peer chain failed on another rank"
+        return False, note if not ok else "peer chain failed on another rank", False
+    try:
+        push_same = run_peer(True) == a
+    except (SpxError, RuntimeError):
+        push_same = False
+    push_ok = all_ok(push_same)
     if same_device:
         Tw, objw, bw = synth.tableau_rows("dense", ms, ns, 99, 0, ms, order="F")
         with DeviceTableau(0) as ref:
@@ -291,14 +316,35 @@ def peer_selftest(eng, world, rank, K, tdist, torch, same_device=False):
         same = (hist.tobytes(), mine.tobytes()) == a
         ok = all_ok(same)
         return ok, ("ok (vs the single-GPU path)" if ok else
-                    "peer chain differs from the single-GPU path")
+                    "peer chain differs from the single-GPU path"), push_ok and ok
     eng.set_chain(1)  # the RCCL all-gather path on the same LP
     eng.load_rows(T, obj, basis, ms, r0)
     eng.solve(**kw)
     same = (eng.history().tobytes(), eng.tableau().tobytes()) == a
-    eng.set_chain(0)
+    eng.set_chain(chain)
     ok = all_ok(same)
-    return ok, "ok" if ok else "peer chain differs from the RCCL path: disabled"
+    return ok, "ok" if ok else "peer chain differs from the RCCL path: disabled", push_ok and ok
+
+
+def select_row_transport(eng, K, opts, windows, world, tdist, torch, push_ok):
+    """Time `windows` windows with each leaving-row transport (pull, then
+    owner-push; the same pivots either way, they continue the run), max over
+    ranks, and let every rank take the same choice (dist.choose_row_transport).
+    Returns (choice, per-transport ms per window, pivots made)."""
+    from simplex_amd.dist import choose_row_transport
+    ms, made = {}, 0
+    for mode in (("pull", "push") if push_ok else ("pull",)):
+        eng.enable_peer_chain(push=(mode == "push"))
+        tdist.barrier()
+        eng.sync()
+        t0 = time.perf_counter()
+        eng.run_pivots(windows * K, **opts)
+        eng.sync()
+        t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
+        tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
+        ms[mode] = 1e3 * float(t.item()) / windows
+        made += windows * K
+    return choose_row_transport(ms["pull"], ms.get("push"), push_ok), ms, made
 
 
 def main():
@@ -341,19 +387,22 @@ def main():
     peer = None
     if args.same_device and not (K and args.peer):
         raise SystemExit("--same-device runs the peer chain only (--window > 1, --peer 1)")
+    push_ok = False
     if world > 1 and K and args.peer:
-        ok, note = peer_selftest(eng, world, rank, K, tdist, torch, args.same_device)
-        peer = {"enabled": ok, "selftest": note}
+        ok, note, push_ok = peer_selftest(eng, world, rank, K, tdist, torch, args.same_device,
+                                          args.chain)
+        peer = {"enabled": ok, "selftest": note, "push_selftest": push_ok}
         if args.same_device and not ok:
             raise SystemExit(f"--same-device: {note}")
-    if world == 1:
+    if world == 1 or (peer is not None and peer["enabled"]):
+        # (at N > 1: the row-sharded chain's block width, modes 0 / 2 / 3)
         eng.set_chain(args.chain, args.chain_blocks)
-    elif peer is None or not peer["enabled"]:
+    else:
         eng.set_chain(1)  # one RCCL all-gather per pivot
     eng.load_rows(Tf, obj, basis, m, row0)
     del Tf
     if peer is not None and peer["enabled"]:
-        eng.enable_peer_chain()
+        eng.enable_peer_chain(push=(args.peer_row == "push" and push_ok))
         if eng.chain_blocks() <= 0:
             raise SystemExit("row-sharded persistent chain passed its self-test but does not fit")
     if args.nt >= 0 or args.ilv >= 0 or args.R or args.wgs or args.fmap >= 0:
@@ -375,6 +424,20 @@ def main():
     # ranks start their first window together: a shard chain waits at most
     # 100 ms at its start handshake for the other ranks' blocks
     barrier()
+    n_trial = 0
+    if peer is not None and peer["enabled"]:
+        if args.peer_row == "auto":
+            # a few windows with each transport (they count as warmup), then
+            # every rank takes the faster one (the same, from all-reduced times)
+            choice, trial, n_trial = select_row_transport(eng, K, dict(
+                rule=args.rule, skip_zero_cols=not args.dense, use_graph=use_graph, chunk=32),
+                args.row_trial, world, tdist, torch, push_ok)
+            peer["row_trial_ms_per_window"] = trial
+        else:
+            choice = "push" if (args.peer_row == "push" and push_ok) else "pull"
+        eng.enable_peer_chain(push=(choice == "push"))
+        peer["row_transport"] = choice
+        barrier()
     eng.run_pivots(n_warm, **opts)
     eng.sync()
     eng.elim_timing(reset=True)
@@ -392,7 +455,7 @@ def main():
         tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
         elapsed = float(t.item())
     status, iters, z = eng.state()
-    if status != 4 or iters != n_warm + n_timed:
+    if status != 4 or iters != n_trial + n_warm + n_timed:
         raise SystemExit(f"pivot loop ended early: status {status}, iters {iters}")
     ms_tot, launches, touched = eng.elim_timing(reset=True)
     chain = None
@@ -499,7 +562,10 @@ def main():
                        "parallelism": ("single GPU" if world == 1 else
                                        f"row-shard x{world}, " + (
                                            "one persistent chain launch per window, ratio "
-                                           "records to every rank + peer row gather (xGMI)"
+                                           "records to every rank + the leaving row "
+                                           + ("pushed by its owner into every peer's inbox"
+                                              if peer.get("row_transport") == "push" else
+                                              "gathered from its owner") + " (xGMI)"
                                            if peer and peer["enabled"] else
                                            "RCCL all-gather of [key | row] per pivot")),
                        "peer_chain": peer},

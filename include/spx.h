@@ -130,8 +130,31 @@ int spx_create_sharded_peer(spx_ctx** out, int device, int rank, int nranks);
  * chains sharing a GPU all resident), else the RCCL path runs. */
 int spx_peer_blob_size(void);
 int spx_peer_export(spx_ctx* ctx, void* out, int64_t cap);
+/* Collective: every rank imports after every rank exported.  The buffers a
+ * context exported are never freed before spx_destroy: a
+ * reload moves them to the context's pool, and later loads of that context
+ * reuse the smallest pooled buffer that fits (at most 4 per buffer role; a
+ * load that would need a fifth fails with SPX_E_STATE -- recreate the
+ * context).  spx_destroy of an exported context waits (bounded, 10 s) for
+ * every peer to release its IPC mapping, so the ranks should destroy
+ * together. */
 int spx_peer_import(spx_ctx* ctx, const void* blobs, int nranks);
 int spx_peer_chain_local(spx_ctx* ctx);
+/* Leaving-row transport of the row-sharded chain, for the next
+ * spx_peer_import / spx_peer_chain_local (every rank must choose the same, or
+ * the import fails): 0 = pull (default; every rank reads the owner's row
+ * through a peer pointer, scattered 8-byte system-scope loads over xGMI),
+ * 1 = owner-push (the owner's blocks write its row contiguously into
+ * every peer's inbox; north_star's "single broadcast of the pivot row").
+ * Bit-identical either way.  spx_get_peer_push: the imported chain's
+ * transport (-1: no peer chain imported). */
+int spx_set_peer_push(spx_ctx* ctx, int on);
+int spx_get_peer_push(spx_ctx* ctx, int* on);
+/* Diagnostic: out[0] this rank's tableau, out[1] its record buffer, out[2]
+ * the import generation, then for every rank q the tableau and record buffer
+ * pointers as mapped here (out[3+2q], out[4+2q]; 0 before an import).
+ * n >= 3 + 2 * nranks. */
+int spx_peer_debug(spx_ctx* ctx, uint64_t* out, int n);
 
 /* ---- data in / out ------------------------------------------------------- */
 /* Load a full tableau of `rows` = m+1 rows (objective row LAST) and `cols` = N
@@ -180,7 +203,17 @@ int spx_pivot_at(spx_ctx* ctx, int64_t r, int64_t c);
  * window whose persistent chain aborted at its start handshake (see
  * spx_set_chain_handshake) is rerun by the next drain of the context
  * (spx_sync, spx_state, a getter, or the next call), so the request still
- * ends after exactly `npivots` pivots. */
+ * ends after exactly `npivots` pivots.  Two duties follow from not waiting:
+ * (1) peer-only row shards (spx_create_sharded_peer) must reach that drain
+ * together -- the rerun is again a cross-rank persistent chain, and a rank
+ * draining much later than its peers (beyond the ~4 s spin bound) leaves
+ * them in ST_FAULT; bench.py and dist.py drain every rank right after the
+ * call, behind a barrier.  (2) The call's persistent-chain admission
+ * (spx_set_chain_budget) is held until that drain, or until another call or
+ * admission decision of this process sees the call's work complete; a
+ * process sharing its GPU with other processes should spx_sync after
+ * spx_run_pivots, else their chains may be refused (and run the slower,
+ * bit-identical launch-per-phase chain) meanwhile. */
 int spx_run_pivots(spx_ctx* ctx, const spx_opts* opts, int64_t npivots, int time_elim);
 /* Wait for the context's enqueued work (and finish an spx_run_pivots request
  * whose window had to be rerun). */
@@ -258,8 +291,10 @@ int spx_get_chain_stats(spx_ctx* ctx, int64_t out[3]);
  * resident (its CU held by another kernel or process, or another chain ahead
  * of it on the same hardware queue), no block stores anything, the window
  * reports ST_NOTRES, and spx_solve / spx_pivot / spx_pivot_at rerun it with
- * the launch-per-phase chain (peer-only shards: the persistent chain again),
- * bit-identical.  us < 0 makes every persistent window abort (test hook). */
+ * the launch-per-phase chain (peer-only shards: the persistent chain again,
+ * giving up after 16 CONSECUTIVE aborts of the same pivot), bit-identical.
+ * us = -k < 0 makes every k-th window (by window epoch) abort; -1 every
+ * window (test hooks). */
 int spx_set_chain_handshake(spx_ctx* ctx, int64_t us);
 /* Windows the context reran after such an abort. */
 int spx_get_chain_reruns(spx_ctx* ctx, int64_t* n);

@@ -34,6 +34,7 @@
 #include <map>
 #include <set>
 #include <mutex>
+#include <thread>
 #include <string>
 #include <vector>
 
@@ -143,10 +144,10 @@ struct spx_ctx {
   // persistent pivot chain of a window (spx_chain.hpp): record buffers and mode
   unsigned long long* gr_enter = nullptr;  // ENTER_REC x CHAIN_MAX_BLOCKS granules
   unsigned long long* gr_ratio = nullptr;  // RATIO_REC x CHAIN_MAX_BLOCKS granules
-  size_t A_bytes = 0, gr_bytes = 0;  // (spx_ctx::kept)
+  size_t A_bytes = 0, gr_bytes = 0;
   int chain_mode = 0;      // 0: persistent chain when it fits, 1: launch per phase
   int chain_min_blocks = 0;
-  int chain_lean = 0;      // chain_kernel<.., LEAN>: no per-slot guards (SPX_CHAIN_LEAN, A/B hook)
+  int chain_lean = 0;      // chain_kernel<.., LEAN> (SPX_CHAIN_LEAN 0..2, A/B hook; spx_chain.hpp)
   // admission of the persistent chain (process-wide block budget per device):
   // blocks this context holds, calls holding them (released by a stream host
   // callback once the call's launches have run), and whether the current call
@@ -163,14 +164,27 @@ struct spx_ctx {
   bool peer_ok = false;
   ChainPeers peers{};
   std::vector<void*> ipc_open;  // IPC-mapped peer buffers (closed on reload / destroy)
-  // Buffers this context exported to peers (spx_peer_export: the tableau and
-  // the record buffer) are not freed before spx_destroy: a reload keeps them
-  // here and reuses one only for a buffer of exactly its size, so a new
-  // allocation never lands at an address a peer has mapped before (an IPC
-  // mapping that a runtime hands back for a recycled address would read freed
-  // or foreign memory).
+  // Exported buffers (round 5).  A buffer this context
+  // exported (spx_peer_export: the tableau, the record buffer) is never freed
+  // before spx_destroy: the IPC export of a NEW allocation at a freed
+  // exported address is not trustworthy on this runtime (round 5: the address
+  // and the handle bytes came back, and the peer's first window faulted;
+  // profiles/r05/ipc/).  A reload puts them in `pool`, tagged by role, and an
+  // allocation of that role takes the smallest pooled buffer that fits, so an
+  // exported address is only ever reused by its own allocation (whose handle
+  // stays valid).  Sizes are rounded up to a class (<= 12.5 % more), and a
+  // role holds at most POOL_MAX buffers: a load needing another fails with
+  // SPX_E_STATE instead of growing.  spx_destroy first waits (bounded) for
+  // every peer's release mark (close_peers), then frees everything.
   bool exported = false;
-  std::vector<std::pair<void*, size_t>> kept;
+  uint32_t peer_gen = 0;        // successful IPC imports of this context (the same on every rank)
+  struct Pooled {
+    void* p;
+    size_t bytes;
+    int role;                   // POOL_TABLEAU / POOL_RECORDS (its allocation flags follow)
+  };
+  std::vector<Pooled> pool;
+  int peer_push = 0;            // leaving-row transport requested for the next import (spx_set_peer_push)
   ChainPeers* d_peers = nullptr;  // device copy of `peers` (the chain kernel's argument)
   int peer_same_dev = 1;        // ranks whose chains share this rank's GPU
   int peer_B = 0, peer_cb = BLK;  // the shard chain's grid, agreed by every rank at import
@@ -180,6 +194,7 @@ struct spx_ctx {
   // after a chain found its blocks not co-resident (ST_NOTRES)
   int64_t hs_us = 0;
   int64_t chain_reruns = 0;
+  int64_t notres_at = -1;   // the iteration count at the last start-handshake abort
   int64_t rp_target = -1;  // iterations the outstanding spx_run_pivots request ends at (-1: none)
   bool st_fresh = false;   // h_st equals the device State (pulled, nothing enqueued since)
 
@@ -244,7 +259,24 @@ void drop_graphs(spx_ctx* ctx) {
   ctx->gexec = nullptr;
 }
 
+// IPC release marks (spx_ctx::exported): granule {CLOSE_TAG, generation} at
+// slot `rank` of each peer's release plane, written through this rank's
+// mapping of that peer's record buffer before the mapping is closed.
+constexpr unsigned CLOSE_TAG = 0xC105ED00u;
+__global__ void peer_release_kernel(const ChainPeers* pe, uint32_t gen) {
+  const int d = threadIdx.x;
+  if (d < pe->nranks && d != pe->rank && pe->ratio[d])
+    g_store<true>((gu64*)pe->ratio[d] + (size_t)CLOSE_PLANE_SHARD * CHAIN_SH_SLOTS + pe->rank,
+                  CLOSE_TAG, gen);
+}
+
 void close_peers(spx_ctx* ctx) {
+  if (!ctx->ipc_open.empty() && ctx->peer_gen > 0 && ctx->d_peers) {
+    // release marks first (the peers' record buffers are still mapped)
+    hipLaunchKernelGGL(peer_release_kernel, dim3(1), dim3(64), 0, ctx->stream,
+                       (const ChainPeers*)ctx->d_peers, ctx->peer_gen);
+    (void)hipStreamSynchronize(ctx->stream);
+  }
   for (void* p : ctx->ipc_open) (void)hipIpcCloseMemHandle(p);
   ctx->ipc_open.clear();
   ctx->peer_ok = false;
@@ -253,16 +285,41 @@ void close_peers(spx_ctx* ctx) {
   ctx->peer_B = 0;
 }
 
+// Every peer's release mark for this context's current import generation, in
+// its own record buffer (bounded wait).  True when all arrived.
+bool wait_peer_release(spx_ctx* ctx, double seconds) {
+  if (ctx->nranks <= 1 || !ctx->gr_ratio) return true;
+  std::vector<unsigned long long> h((size_t)ctx->nranks);
+  const auto t0 = std::chrono::steady_clock::now();
+  for (;;) {
+    if (hipMemcpy(h.data(), ctx->gr_ratio + (size_t)CLOSE_PLANE_SHARD * CHAIN_SH_SLOTS,
+                  sizeof(unsigned long long) * h.size(), hipMemcpyDeviceToHost) != hipSuccess)
+      return false;
+    bool all = true;
+    for (int q = 0; q < ctx->nranks; ++q)
+      if (q != ctx->rank)
+        all &= (unsigned)(h[q] >> 32) == CLOSE_TAG && (uint32_t)h[q] == ctx->peer_gen;
+    if (all) return true;
+    if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > seconds)
+      return false;
+    std::this_thread::sleep_for(std::chrono::microseconds(200));
+  }
+}
+
+// Frees the loaded tableau's buffers; an exported tableau and record buffer
+// go to the context's pool instead (spx_ctx::pool).
+constexpr int POOL_TABLEAU = 0, POOL_RECORDS = 1, POOL_MAX = 4;
 int free_buffers(spx_ctx* ctx) {
   drop_graphs(ctx);
   close_peers(ctx);
-  if (ctx->exported) {  // (see spx_ctx::kept)
-    if (ctx->A) ctx->kept.emplace_back(ctx->A, ctx->A_bytes);
-    if (ctx->gr_ratio) ctx->kept.emplace_back(ctx->gr_ratio, ctx->gr_bytes);
+  const char* keep = std::getenv("SPX_IPC_KEEP");  // diagnostic: 0 = free them (unsafe)
+  if (ctx->exported && !(keep && keep[0] == '0')) {
+    if (ctx->A) ctx->pool.push_back({ctx->A, ctx->A_bytes, POOL_TABLEAU});
+    if (ctx->gr_ratio) ctx->pool.push_back({ctx->gr_ratio, ctx->gr_bytes, POOL_RECORDS});
     ctx->A = nullptr;
     ctx->gr_ratio = nullptr;
-    ctx->exported = false;
   }
+  ctx->exported = false;
   dfree(ctx->A);
   dfree(ctx->obj);
   dfree(ctx->F);
@@ -286,6 +343,51 @@ int free_buffers(spx_ctx* ctx) {
   dfree(ctx->gr_enter);
   dfree(ctx->gr_ratio);
   ctx->loaded = false;
+  return SPX_OK;
+}
+
+// Size class of a pooled role: up to 1/8 more, in 2 MiB steps at least, so a
+// pooled buffer serves the sizes near it.
+size_t pool_class(size_t bytes) {
+  size_t g = (size_t)2 << 20;
+  while ((g << 4) <= bytes) g <<= 1;  // g ~ bytes / 8 .. bytes / 16
+  return (bytes + g - 1) / g * g;
+}
+
+// A buffer of `role` for `bytes`: the smallest pooled one that fits, else a
+// new allocation of the role's class (records of multi-process shards are
+// uncached).  *got = its size.  SPX_E_STATE when the role's pool is full.
+int pool_take(spx_ctx* ctx, int role, size_t bytes, bool uncached, void** out, size_t* got) {
+  int best = -1;
+  int held = 0;
+  for (int x = 0; x < (int)ctx->pool.size(); ++x) {
+    const auto& e = ctx->pool[x];
+    if (e.role != role) continue;
+    ++held;
+    if (e.bytes >= bytes && (best < 0 || e.bytes < ctx->pool[best].bytes)) best = x;
+  }
+  if (best >= 0) {
+    *out = ctx->pool[best].p;
+    *got = ctx->pool[best].bytes;
+    ctx->pool.erase(ctx->pool.begin() + best);
+    return SPX_OK;
+  }
+  if (held >= POOL_MAX) {
+    ctx->err = "a peer-chain shard reloaded with more distinct sizes than its pool of exported "
+               "buffers holds (4 per role; they are never freed before spx_destroy, DESIGN.md "
+               "5c): destroy and recreate the context";
+    return SPX_E_STATE;
+  }
+  const size_t sz = pool_class(bytes);
+  if (uncached) {
+    if (hipExtMallocWithFlags(out, sz, hipDeviceMallocUncached) != hipSuccess) {
+      (void)hipGetLastError();
+      HIPC(hipMalloc(out, sz));
+    }
+  } else {
+    HIPC(hipMalloc(out, sz));
+  }
+  *got = sz;
   return SPX_OK;
 }
 
@@ -614,7 +716,13 @@ int shm_fd_locked(ChainAdmission& a, int device) {
   t.fd = -1;
   if (!shm_enabled()) return -1;
   if (t.path.empty()) t.path = shm_path(device);
-  t.fd = open(t.path.c_str(), O_RDWR | O_CREAT | O_CLOEXEC, 0666);
+  // (no symlink followed; only a regular file is used as the table)
+  t.fd = open(t.path.c_str(), O_RDWR | O_CREAT | O_CLOEXEC | O_NOFOLLOW, 0666);
+  struct stat sb;
+  if (t.fd >= 0 && (fstat(t.fd, &sb) != 0 || !S_ISREG(sb.st_mode))) {
+    close(t.fd);
+    t.fd = -1;
+  }
   // every process (user) on the GPU shares the table: 0666 regardless of the
   // umask (fchmod, not a process-wide umask change; fails harmlessly when
   // another user created the file)
@@ -638,14 +746,15 @@ int shm_exchange(int fd, int mine, Admit admit, bool* ok = nullptr) {
   const ssize_t got = pread(fd, e, sizeof(e), 0);
   (void)got;  // (a short or new file reads as free entries)
   const int32_t me = (int32_t)getpid();
-  int others = 0, slot = -1, free_slot = -1;
+  int64_t others = 0;  // (entries are untrusted: each clamped, summed in 64 bits)
+  int slot = -1, free_slot = -1;
   bool dirty = false;
   for (int x = 0; x < SHM_SLOTS; ++x) {
     if (e[x].pid == me) {
       slot = x;
     } else if (e[x].pid > 0 && e[x].blocks > 0) {
       if (shm_entry_live(e[x])) {
-        others += e[x].blocks;
+        others += std::min<int64_t>(e[x].blocks, CHAIN_MAX_BLOCKS);
       } else {  // a dead process's entry (or its pid reused): free it
         e[x] = ShmEntry{0, 0, 0};
         dirty = true;
@@ -653,7 +762,7 @@ int shm_exchange(int fd, int mine, Admit admit, bool* ok = nullptr) {
     }
     if (free_slot < 0 && (e[x].pid <= 0 || e[x].blocks <= 0) && e[x].pid != me) free_slot = x;
   }
-  const bool go = admit(others);
+  const bool go = admit((int)std::min<int64_t>(others, INT32_MAX / 2));
   if (ok) *ok = go;
   if (go && mine >= 0) {
     if (slot < 0) slot = free_slot;
@@ -664,7 +773,7 @@ int shm_exchange(int fd, int mine, Admit admit, bool* ok = nullptr) {
   }
   if (dirty) (void)!pwrite(fd, e, sizeof(e), 0);
   flock(fd, LOCK_UN);
-  return others;
+  return (int)std::min<int64_t>(others, INT32_MAX / 2);
 }
 int shm_set(int fd, int mine) {
   return shm_exchange(fd, mine, [](int) { return true; });
@@ -815,7 +924,8 @@ int enqueue_window_t(spx_ctx* ctx, int npiv, bool time_flush) {
                                           : chain_shard_kernel<KMAX, 256>)
                              : (cb == 512 ? chain_kernel<KMAX, 512> : chain_kernel<KMAX, 256>);
     if constexpr (KMAX % 4 == 0)
-      if (!ctx->sharded && cb == 256 && ctx->chain_lean) kern = chain_kernel<KMAX, 256, true>;
+      if (!ctx->sharded && cb == 256 && ctx->chain_lean)
+        kern = ctx->chain_lean == 1 ? chain_kernel<KMAX, 256, 1> : chain_kernel<KMAX, 256, 2>;
     hipLaunchKernelGGL(kern, dim3(B), dim3(cb), 0, ctx->stream, ctx->enter_part, ctx->st,
                        (const Params*)ctx->prm, std::max(NWAVE * ctx->nbn, B),
                        (const double*)ctx->A, ctx->ld, ctx->m_local, ctx->N, ctx->obj, ctx->win,
@@ -983,7 +1093,7 @@ int make_params(spx_ctx* ctx, const spx_opts* o, Params* out) {
 // chain may start that much after another's); spx_set_chain_handshake
 // overrides it (< 0: every persistent window aborts, a test hook).
 int64_t hs_ticks(const spx_ctx* ctx) {
-  if (ctx->hs_us < 0) return -1;
+  if (ctx->hs_us < 0) return ctx->hs_us;  // -k: abort every k-th window (chain_start; test hook)
   if (ctx->hs_us > 0) return ctx->hs_us * 100;
   return ctx->sharded ? 10000000 : 2000;
 }
@@ -1115,6 +1225,11 @@ constexpr int NOTRES_RETRIES = 16;
 int notres_resume(spx_ctx* ctx, int64_t fc, int64_t fr, int* retries) {
   ctx->chain_reruns++;
   const bool lazy_ok = !ctx->sharded || ctx->comm || ctx->loop;
+  // only CONSECUTIVE aborts count (the same pivot aborted again and again): a
+  // long solve with sporadic aborts, each rerun successfully, never gives up
+  // (ctx->h_st is current: every caller pulled the State first)
+  if (ctx->h_st->iters != ctx->notres_at) *retries = 0;
+  ctx->notres_at = ctx->h_st->iters;
   if (!lazy_ok && ++*retries > NOTRES_RETRIES) {
     ctx->err = "persistent chain: blocks not co-resident after repeated reruns (peer-only "
                "shard: no launch-per-phase path)";
@@ -1162,17 +1277,6 @@ int rp_recover(spx_ctx* ctx) {
   }
 }
 
-// A kept (once exported) buffer of exactly `bytes`, if any (spx_ctx::kept).
-bool take_kept(spx_ctx* ctx, size_t bytes, void** out) {
-  for (auto it = ctx->kept.begin(); it != ctx->kept.end(); ++it)
-    if (it->second == bytes) {
-      *out = it->first;
-      ctx->kept.erase(it);
-      return true;
-    }
-  return false;
-}
-
 int alloc_common(spx_ctx* ctx, int64_t m_local, int64_t N, int64_t m_global, int64_t row0) {
   free_buffers(ctx);
   ctx->m_local = m_local;
@@ -1185,8 +1289,15 @@ int alloc_common(spx_ctx* ctx, int64_t m_local, int64_t N, int64_t m_global, int
   ctx->hist_cap = 1 << 20;
   HIPC(hipSetDevice(ctx->device));
   ctx->A_bytes = sizeof(double) * ctx->ld * N;
-  if (!take_kept(ctx, ctx->A_bytes, reinterpret_cast<void**>(&ctx->A)))
+  // (the buffers a row shard may export come from its pool, spx_ctx::pool)
+  const bool exportable = ctx->sharded && !ctx->loop;
+  if (exportable) {
+    if (const int rc = pool_take(ctx, POOL_TABLEAU, ctx->A_bytes, false,
+                                 reinterpret_cast<void**>(&ctx->A), &ctx->A_bytes))
+      return rc;
+  } else {
     HIPC(hipMalloc(&ctx->A, ctx->A_bytes));
+  }
   HIPC(hipMalloc(&ctx->obj, sizeof(double) * N));
   HIPC(hipMalloc(&ctx->F, sizeof(double) * 2 * ctx->ld));
   HIPC(hipMalloc(&ctx->P, sizeof(double) * N));
@@ -1219,18 +1330,17 @@ int alloc_common(spx_ctx* ctx, int64_t m_local, int64_t N, int64_t m_global, int
     // (peers write them over xGMI: uncached, so this GPU's L2 never serves a
     // stale copy to the local polls; plain memory between virtual ranks)
     // (+2 planes: the start handshake's arrivals and verdict word)
+    // (+2 planes: the start handshake's arrivals and verdict word; shards also
+    // the IPC release plane and the owner-push inbox, spx_chain.hpp)
     const size_t gq = sizeof(unsigned long long) *
-                      (ctx->sharded ? (size_t)(HS_PLANE_SHARD + 2) * CHAIN_SH_SLOTS
+                      (ctx->sharded ? (size_t)shard_record_granules(N)
                                     : (size_t)(HS_PLANE_1GPU + 2) * CHAIN_MAX_BLOCKS);
     HIPC(hipMalloc(&ctx->gr_enter, ge));
     ctx->gr_bytes = gq;
-    if (take_kept(ctx, gq, reinterpret_cast<void**>(&ctx->gr_ratio))) {
-      // (a kept record buffer: allocated as below by an earlier load)
-    } else if (ctx->sharded && !ctx->loop) {
-      if (hipExtMallocWithFlags((void**)&ctx->gr_ratio, gq, hipDeviceMallocUncached) != hipSuccess) {
-        (void)hipGetLastError();
-        HIPC(hipMalloc(&ctx->gr_ratio, gq));
-      }
+    if (exportable) {
+      if (const int rc = pool_take(ctx, POOL_RECORDS, gq, true,
+                                   reinterpret_cast<void**>(&ctx->gr_ratio), &ctx->gr_bytes))
+        return rc;
     } else {
       HIPC(hipMalloc(&ctx->gr_ratio, gq));
     }
@@ -1304,7 +1414,8 @@ int spx_create(spx_ctx** out, int device) {
   if (const char* ft = std::getenv("SPX_FLUSH_TAIL"))
     ctx->flush_tail = std::max(0, std::min(50, std::atoi(ft)));
   // the single-GPU chain's LEAN slot chains (0 / 1; A/B hook, spx_chain.hpp)
-  if (const char* cl = std::getenv("SPX_CHAIN_LEAN")) ctx->chain_lean = std::atoi(cl) != 0;
+  if (const char* cl = std::getenv("SPX_CHAIN_LEAN"))
+    ctx->chain_lean = std::max(0, std::min(2, std::atoi(cl)));
   // windows per replayed graph (1..16; tuning hook)
   if (const char* gw = std::getenv("SPX_GRAPH_WINDOWS"))
     ctx->graph_windows = std::max(1, std::min(16, std::atoi(gw)));
@@ -1389,16 +1500,16 @@ struct PeerBlob {
   hipIpcMemHandle_t hA, hR;  // this rank's tableau and ratio-record buffer
   int64_t ld, row0, m_local, N, m_global;
   char bus[64];              // PCI bus id: which ranks share a GPU
-  int32_t n_cu, chain_mode, chain_min_blocks, pad;  // what the shard geometry depends on
+  int32_t n_cu, chain_mode, chain_min_blocks, push;  // what the shard geometry depends on
 };
-constexpr uint32_t PEER_MAGIC = 0x53505851u;  // "SPXQ" (round 4 layout)
+constexpr uint32_t PEER_MAGIC = 0x53505852u;  // "SPXR" (round 5: + the row transport)
 
 // What one rank contributes to the shard chain's geometry (its blob, or a
 // virtual rank's context): every rank computes the geometry from ALL ranks'
 // inputs, in rank order, so every rank reaches the same decision.
 struct ShardIn {
   std::string dev;  // device key (PCI bus id): the ranks sharing a GPU form a group
-  int n_cu = 0, mode = 0, min_blocks = 0;
+  int n_cu = 0, mode = 0, min_blocks = 0, push = 0;
   int64_t m_local = 0;
 };
 
@@ -1411,9 +1522,13 @@ struct ShardIn {
 int shard_geometry(spx_ctx* ctx, ChainPeers& pe, const std::vector<ShardIn>& in, int* B_out,
                    int* cb_out) {
   const int nr = pe.nranks;
-  for (int q = 1; q < nr; ++q)
+  for (int q = 1; q < nr; ++q) {
     CHECK_ARG(in[q].mode == in[0].mode && in[q].min_blocks == in[0].min_blocks,
               "peer chain: ranks disagree on the chain mode (spx_set_chain)");
+    CHECK_ARG(in[q].push == in[0].push,
+              "peer chain: ranks disagree on the leaving-row transport (spx_set_peer_push)");
+  }
+  pe.push = in[0].push;
   pe.ngroups = 0;
   int gof[CHAIN_MAX_RANKS];
   for (int q = 0; q < nr; ++q) {
@@ -1502,6 +1617,7 @@ int spx_peer_export(spx_ctx* ctx, void* out, int64_t cap) {
   b.n_cu = ctx->n_cu;
   b.chain_mode = ctx->chain_mode;
   b.chain_min_blocks = ctx->chain_min_blocks;
+  b.push = ctx->peer_push;
   std::memcpy(out, &b, sizeof(b));
   return SPX_OK;
 }
@@ -1534,6 +1650,7 @@ int spx_peer_import(spx_ctx* ctx, const void* blobs, int nranks) {
     in[q].n_cu = b.n_cu;
     in[q].mode = b.chain_mode;
     in[q].min_blocks = b.chain_min_blocks;
+    in[q].push = b.push;
     in[q].m_local = b.m_local;
   }
   CHECK_ARG(rows_sum == ctx->m_global, "peer import: the row blocks do not cover every row");
@@ -1562,7 +1679,9 @@ int spx_peer_import(spx_ctx* ctx, const void* blobs, int nranks) {
     pe.A[q] = static_cast<const double*>(pa);
     pe.ratio[q] = static_cast<unsigned long long*>(pr);
   }
-  return peer_commit(ctx, pe, B, cb);
+  if ((rc = peer_commit(ctx, pe, B, cb))) return rc;
+  ctx->peer_gen++;  // (every rank imports together: the same generation everywhere)
+  return SPX_OK;
 }
 
 // Virtual ranks (spx_create_sharded_local): the peers are this process's
@@ -1600,6 +1719,7 @@ int spx_peer_chain_local(spx_ctx* ctx) {
     in[q].n_cu = device_cus(m->device);
     in[q].mode = m->chain_mode;
     in[q].min_blocks = m->chain_min_blocks;
+    in[q].push = m->peer_push;
     in[q].m_local = m->m_local;
   }
   CHECK_ARG(rows_sum == ctx->m_global, "spx_peer_chain_local: row blocks do not cover every row");
@@ -1634,10 +1754,15 @@ int spx_destroy(spx_ctx* ctx) {
     while (ctx->adm_calls > 0) adm_release_locked(a, ctx);  // (error paths)
   }
   if (ctx->adm_ev) (void)hipEventDestroy(ctx->adm_ev);
-  ctx->exported = false;  // (destroy: the exported buffers go too)
+  // the peers' release marks (close_peers) for this context's exported
+  // buffers, a bounded wait, then every buffer goes
+  const bool was_exported = ctx->exported || !ctx->pool.empty();
+  close_peers(ctx);
+  if (was_exported && ctx->peer_gen > 0) (void)wait_peer_release(ctx, 10.0);
+  ctx->exported = false;
+  for (const auto& e : ctx->pool) (void)hipFree(e.p);
+  ctx->pool.clear();
   free_buffers(ctx);
-  for (auto& k : ctx->kept) (void)hipFree(k.first);
-  ctx->kept.clear();
   for (auto* pool : {&ctx->ev, &ctx->evc})
     for (auto& e : *pool) {
       (void)hipEventDestroy(e.first);
@@ -2269,6 +2394,39 @@ int spx_set_chain_handshake(spx_ctx* ctx, int64_t us) {
 int spx_get_chain_reruns(spx_ctx* ctx, int64_t* n) {
   if (!ctx || !n) return SPX_E_ARG;
   *n = ctx->chain_reruns;
+  return SPX_OK;
+}
+
+// Leaving-row transport of the row-sharded chain for the next
+// spx_peer_import / spx_peer_chain_local: 0 pull, 1 owner-push.
+int spx_set_peer_push(spx_ctx* ctx, int on) {
+  if (!ctx) return SPX_E_ARG;
+  CHECK_ARG(on == 0 || on == 1, "peer push must be 0 (pull) or 1 (owner-push)");
+  ctx->peer_push = on;
+  return SPX_OK;
+}
+
+// The transport of the imported peer chain (-1: none imported).
+int spx_get_peer_push(spx_ctx* ctx, int* on) {
+  if (!ctx || !on) return SPX_E_ARG;
+  *on = ctx->peer_ok ? ctx->peers.push : -1;
+  return SPX_OK;
+}
+
+// Diagnostic: this rank's exported buffers and the peer
+// pointers it imported.  out[0] tableau, out[1] record buffer, out[2] import
+// generation, then per rank q < nranks: out[3 + 2q] tableau, out[4 + 2q]
+// record buffer as mapped here (0 when not imported).
+int spx_peer_debug(spx_ctx* ctx, uint64_t* out, int n) {
+  if (!ctx || !out) return SPX_E_ARG;
+  CHECK_ARG(n >= 3 + 2 * ctx->nranks, "spx_peer_debug: out too small");
+  out[0] = (uint64_t)(uintptr_t)ctx->A;
+  out[1] = (uint64_t)(uintptr_t)ctx->gr_ratio;
+  out[2] = ctx->peer_gen;
+  for (int q = 0; q < ctx->nranks; ++q) {
+    out[3 + 2 * q] = ctx->peer_ok ? (uint64_t)(uintptr_t)ctx->peers.A[q] : 0;
+    out[4 + 2 * q] = ctx->peer_ok ? (uint64_t)(uintptr_t)ctx->peers.ratio[q] : 0;
+  }
   return SPX_OK;
 }
 

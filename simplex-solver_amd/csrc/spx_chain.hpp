@@ -118,6 +118,19 @@ constexpr int CHAIN_SH_PLANES = 2 * RATIO_REC + 1;
 // rank that leads the caller's device group.
 constexpr int HS_PLANE_1GPU = RATIO_REC;
 constexpr int HS_PLANE_SHARD = CHAIN_SH_PLANES;
+// Row shards, after the handshake planes: one plane of IPC release marks
+// (spx_capi.hip close_peers: slot q = rank q's mapping of this buffer is
+// closed, value = the import generation), then the owner-push inbox.
+constexpr int CLOSE_PLANE_SHARD = HS_PLANE_SHARD + 2;
+constexpr int INBOX_PLANE_SHARD = HS_PLANE_SHARD + 3;
+// Owner-push inbox (round 5): the leaving row's stale values,
+// pushed by its owner into every peer's buffer as tagged granules: [half by
+// pivot parity][low word, high word][column], each plane inbox_stride(N)
+// granules.
+__host__ __device__ constexpr int64_t inbox_stride(int64_t N) { return (N + 63) / 64 * 64; }
+__host__ __device__ constexpr int64_t shard_record_granules(int64_t N) {
+  return (int64_t)INBOX_PLANE_SHARD * CHAIN_SH_SLOTS + 4 * inbox_stride(N);
+}
 
 typedef __attribute__((address_space(1))) unsigned long long gu64;
 typedef __attribute__((address_space(1))) unsigned gu32;
@@ -145,6 +158,10 @@ struct ChainPeers {
   int64_t ld[CHAIN_MAX_RANKS];
   int64_t row0[CHAIN_MAX_RANKS];
   const int32_t* stop_req;  // rank 0: the host's time-limit stop request (pinned)
+  // leaving-row transport: 0 pull (every rank reads the owner's tableau
+  // through a peer pointer), 1 owner-push (the owner writes the row into every
+  // peer's inbox); agreed by every rank at import
+  int push;
   // device groups (ranks sharing a GPU) for the start handshake: group g's
   // lowest rank gleader[g] holds its arrival plane and verdict word; gmask[g]
   // has a bit per member rank; `group` is this rank's
@@ -340,7 +357,10 @@ __device__ __forceinline__ int chain_start(const gu64* arr, int nslots, int B, u
                                            uint64_t t0, const ChainPeers* pe, State* st) {
   const int lane = threadIdx.x & 63;
   const unsigned tag = rec_tag(W, 0, GK_START);
-  bool late = bound < 0;  // (a negative bound forces ABORT: the rerun test hook)
+  // a negative bound -k forces ABORT of every k-th window epoch (k = 1: every
+  // window; the rerun test hooks); the others wait the automatic bound
+  bool late = bound < 0 && (W % (uint32_t)(-bound)) == 0u;
+  if (bound < 0) bound = SYS ? 10000000 : 2000;
   for (unsigned spins = 0; !late;) {
     bool ok = true;
     for (int x = lane; x < nslots; x += 64)
@@ -654,7 +674,7 @@ __device__ __forceinline__ double sys_load(const double* p) {
 // written by the previous kernel (norm<INIT> or the previous window's chain);
 // the chain writes one partial per block there for the next window.
 // ---------------------------------------------------------------------------
-template <int KMAX, int CB, bool LEAN = false>
+template <int KMAX, int CB, int LEAN = 0>
 __global__ __launch_bounds__(CB) void chain_kernel(
     Key* __restrict__ enter_part, State* st, const Params* __restrict__ prm, int n_ep,
     const double* __restrict__ A, int64_t ld, int64_t m, int64_t N, double* __restrict__ obj,
@@ -667,7 +687,12 @@ __global__ __launch_bounds__(CB) void chain_kernel(
   // "s < q" select.  A slot s >= q is an exact identity instead: its f and p
   // histories are +0 (LDS zeroed at the window start, record lanes >= q are
   // +0), and v - (+0 * +0) = v for every v, -0 and NaN included.  Only a
-  // chunk of CH slots is guarded, by a uniform branch.
+  // chunk of CH slots is guarded, by a uniform branch.  LEAN >= 2 also runs
+  // the norm phase's zero-p slots (skip rule, zmask) on that fast chain: p is
+  // taken as +0 there, and v - (f * +0) = v for every finite f unless v = -0
+  // (a chain value can only be -0 when the stale value is), so a wave takes
+  // it when no lane has an entered column (cmask), a -0 stale value with a
+  // zero slot, or a non-finite f.
   constexpr int CH = LEAN ? 4 : KMAX % 8 == 0 ? 8 : KMAX % 4 == 0 ? 4 : 2;
   // LH: the window histories f_s[i] (rows) and p_s[j] (columns) live in LDS,
   // slot-major, one column per thread: a phase reads its thread's slots once
@@ -977,6 +1002,10 @@ __global__ __launch_bounds__(CB) void chain_kernel(
 #pragma unroll
       for (int s = 0; s < KMAX; ++s) ps[s] = psl[s][t];
     }
+    if constexpr (LEAN >= 2) {  // zero-p slots as +0 (the records keep psl's values)
+#pragma unroll
+      for (int s = 0; s < KMAX; ++s) ps[s] = ((zmask >> s) & 1u) ? 0.0 : ps[s];
+    }
     double frl = 0.0, ex[2];
     if (!load_extras<1>(gr_ratio, wb, RATIO_HDR + 2, q + 1, RATIO_HDR, rec_tag(W, q, GK_RATIO),
                         frl, ex, st))
@@ -994,7 +1023,14 @@ __global__ __launch_bounds__(CB) void chain_kernel(
     // see (piv * +0 may be -0); lanes > q are +0 already
     const double frm = LEAN ? (lane < q ? frl : 0.0) : frl;
     if (__ballot(lane < q && slot_r == r) == 0ull) {
-      if (__ballot(jlive && ((zmask | cmask) & qmn) != 0u) == 0ull) {
+      bool fast = __ballot(jlive && ((zmask | cmask) & qmn) != 0u) == 0ull;
+      if constexpr (LEAN >= 2)
+        fast = fast ||
+               (__ballot(jlive && (cmask & qmn) != 0u) == 0ull &&
+                __ballot(jlive && (zmask & qmn) != 0u &&
+                         __double_as_longlong(v) == (long long)0x8000000000000000ull) == 0ull &&
+                __ballot(lane < q && !__builtin_isfinite(frl)) == 0ull);
+      if (fast) {
 #pragma unroll
         for (int c8 = 0; c8 < KMAX; c8 += CH) {
           if (c8 < q) {
@@ -1269,6 +1305,8 @@ __global__ __launch_bounds__(CB) void chain_shard_kernel(
   constexpr int RS = CHAIN_SH_SLOTS;
   const int BR = nr * B;
   const int bs = rank * B + b;
+  const bool push = pe->push != 0;
+  const int64_t NI = inbox_stride(N);
   // rank 0's time-limit stop request rides in its ratio records (bit 31 of
   // granule 3); read once per window, so every rank stops at the window's start
   const unsigned stopbit =
@@ -1281,6 +1319,10 @@ __global__ __launch_bounds__(CB) void chain_shard_kernel(
   // has read ratio q; never q + 2)
   auto ratio_buf = [&](int d, int qq) -> gu64* {
     return (gu64*)pe->ratio[d] + (size_t)((it0 + qq) & 1) * RATIO_REC * RS;
+  };
+  // rank d's inbox half for pivot it0 + qq (owner-push): low words, then high
+  auto inbox = [&](int d, int qq) -> gu64* {
+    return (gu64*)pe->ratio[d] + (size_t)INBOX_PLANE_SHARD * RS + (size_t)((it0 + qq) & 1) * 2 * NI;
   };
   (void)gr_ratio;
   // my column and my row
@@ -1545,18 +1587,46 @@ __global__ __launch_bounds__(CB) void chain_shard_kernel(
     }
     // row r on my column: stale + pending slots.  f_s[r] (lane s <= q, lane q
     // the pivot element) and the row's RHS from the winning ratio record
-    double v;  // the owner's stale row (a peer's tableau unless it is mine)
+    double v = 0.0;  // the owner's stale row (a peer's tableau unless it is mine)
     const int own = wb / B;
+    const unsigned rtag = rec_tag(W, q, GK_RATIO);
     if (own == rank) v = A[jc * ld + (r - row0)];
-    else v = sys_load(pe->A[own] + jc * pe->ld[own] + (r - pe->row0[own]));
+    else if (!push) v = sys_load(pe->A[own] + jc * pe->ld[own] + (r - pe->row0[own]));
     if constexpr (LH) {  // my column's p history, read while the gathers are in flight
 #pragma unroll
       for (int s = 0; s < KMAX; ++s) ps[s] = psl[s][t];
     }
     double frl = 0.0, ex[2];
     if (!load_extras<1, true, RS>(ratio_buf(rank, q), wb, RATIO_HDR + 2, q + 1, RATIO_HDR,
-                            rec_tag(W, q, GK_RATIO), frl, ex, st))
+                            rtag, frl, ex, st))
       return;
+    if (push) {
+      if (own == rank) {
+        // owner-push: my stale row values into every peer's inbox (contiguous
+        // granules per column block; the data is the flag, no fence)
+        if (jlive) {
+          const unsigned long long x = (unsigned long long)__double_as_longlong(v);
+          for (int d = 0; d < nr; ++d) {
+            if (d == rank) continue;
+            gu64* ib = inbox(d, q);
+            g_store<true>(ib + jc, rtag, (unsigned)x);
+            g_store<true>(ib + NI + jc, rtag, (unsigned)(x >> 32));
+          }
+        }
+      } else {
+        // the owner's push into my inbox: every lane's two granules tagged
+        const gu64* ib = inbox(rank, q);
+        for (unsigned spins = 0;;) {
+          const unsigned long long lo = g_load<true>(ib + jc), hi = g_load<true>(ib + NI + jc);
+          const bool good = !jlive || ((unsigned)(lo >> 32) == rtag && (unsigned)(hi >> 32) == rtag);
+          if (__all(good)) {
+            v = jlive ? g_decode_d(lo, hi) : 0.0;
+            break;
+          }
+          if (spin_fail(spins, st)) return;
+        }
+      }
+    }
     SPX_PROBE(q, 3, 0, v != 12345.678 && frl != 12345.678);  // loads arrived
     const double piv = rdlane(frl, q);
     prhs = ex[0] / piv;  // p_q[rhs]: lazy_norm's p = v / piv of the RHS column
@@ -1717,7 +1787,9 @@ __global__ __launch_bounds__(CB) void chain_shard_kernel(
     // consumed before the last block barrier above); block 0 of every rank
     // waits for all nr * B reports, so no rank's chain launch completes
     // before every rank is done reading.
-    if (w0) {
+    // (owner-push: no rank reads another's rows, so no barrier is needed; the
+    // inbox halves by pivot parity keep a rank running a slot ahead safe)
+    if (w0 && !push) {
       const unsigned dtag = rec_tag(W, 0, GK_DONE);
       if (lane < nr)
         g_store<true>((gu64*)pe->ratio[lane] + (size_t)2 * RATIO_REC * RS + bs, dtag, 0u);

@@ -110,6 +110,9 @@ SIGNATURES = {
     "spx_peer_export": (ctypes.c_int, [_P, ctypes.c_void_p, _I64]),
     "spx_peer_import": (ctypes.c_int, [_P, ctypes.c_char_p, ctypes.c_int]),
     "spx_peer_chain_local": (ctypes.c_int, [_P]),
+    "spx_set_peer_push": (ctypes.c_int, [_P, ctypes.c_int]),
+    "spx_get_peer_push": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_int)]),
+    "spx_peer_debug": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_uint64), ctypes.c_int]),
     "spx_get_chain_stats": (ctypes.c_int, [_P, _LP]),
     "spx_set_chain_handshake": (ctypes.c_int, [_P, _I64]),
     "spx_chain_shm_path": (ctypes.c_int, [ctypes.c_int, ctypes.c_char_p, ctypes.c_int]),

@@ -40,6 +40,16 @@ def row_partition(m: int, world: int, rank: int) -> tuple:
     return row0, row0 + base + (1 if rank < extra else 0)
 
 
+def choose_row_transport(ms_pull: float, ms_push: float | None, push_ok: bool = True) -> str:
+    """The leaving-row transport of the row-sharded chain, from a short timed
+    trial of each (bench.py): "push" when its self-test passed and its windows
+    ran faster, else "pull".  Every rank passes the same (all-reduced) times,
+    so every rank makes the same choice."""
+    if push_ok and ms_push is not None and ms_push < ms_pull:
+        return "push"
+    return "pull"
+
+
 def make_unique_id() -> bytes:
     buf = ctypes.create_string_buffer(128)
     rc = L.lib().spx_comm_unique_id(buf)
@@ -71,13 +81,19 @@ class ShardedTableau(DeviceTableau):
         super().__init__(device, _sharded=(rank, world, uid, local))
         self.rank, self.world, self.local = rank, world, local
 
-    def enable_peer_chain(self, allgather=None) -> None:
+    def enable_peer_chain(self, allgather=None, push: bool | None = None) -> None:
         """Set up the row-sharded persistent chain for the loaded rows (DESIGN.md
         §5): every rank calls this after its load.  Virtual ranks meet in
         process; otherwise this rank's blob (IPC handles of its tableau and
         record buffer) is all-gathered with `allgather(bytes) -> list[bytes]`
-        (default: torch.distributed.all_gather_object) and imported."""
+        (default: torch.distributed.all_gather_object) and imported.
+        push: the leaving-row transport (None: keep the context's setting;
+        False pull from the owner's tableau, True owner-push into every peer's
+        inbox; every rank must pass the same).  Calling it again re-imports,
+        e.g. to switch the transport between windows."""
         lib = self._lib
+        if push is not None:
+            self.set_peer_push(push)
         if self.local is True:
             self._check(lib.spx_peer_chain_local(self._ctx), "spx_peer_chain_local")
             return
@@ -96,6 +112,26 @@ class ShardedTableau(DeviceTableau):
             raise RuntimeError("peer chain: bad blob exchange")
         self._check(lib.spx_peer_import(self._ctx, b"".join(blobs), self.world),
                     "spx_peer_import")
+
+    def set_peer_push(self, on: bool) -> None:
+        """Leaving-row transport for the next enable_peer_chain (spx_set_peer_push)."""
+        self._check(self._lib.spx_set_peer_push(self._ctx, 1 if on else 0), "spx_set_peer_push")
+
+    def peer_push(self) -> int:
+        """The imported peer chain's transport: 0 pull, 1 push, -1 none."""
+        v = ctypes.c_int()
+        self._check(self._lib.spx_get_peer_push(self._ctx, ctypes.byref(v)), "spx_get_peer_push")
+        return int(v.value)
+
+    def peer_debug(self) -> dict:
+        """Diagnostic: this rank's exported buffers, the import generation and
+        the peer pointers it mapped (spx_peer_debug)."""
+        n = 3 + 2 * self.world
+        out = (ctypes.c_uint64 * n)()
+        self._check(self._lib.spx_peer_debug(self._ctx, out, n), "spx_peer_debug")
+        return {"A": out[0], "records": out[1], "gen": out[2],
+                "peer_A": [out[3 + 2 * q] for q in range(self.world)],
+                "peer_records": [out[4 + 2 * q] for q in range(self.world)]}
 
     @classmethod
     def from_env(cls, device: int | None = None, group=None) -> "ShardedTableau":

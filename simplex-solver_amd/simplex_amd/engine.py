@@ -342,8 +342,9 @@ class DeviceTableau:
 
     def set_chain_handshake(self, us: int = 0) -> None:
         """Start-handshake bound of persistent chains in us (0: automatic,
-        20 us on one GPU / 100 ms for row shards; < 0: every persistent window
-        aborts and is rerun -- a test hook).  spx_set_chain_handshake."""
+        20 us on one GPU / 100 ms for row shards; -k < 0: every k-th window
+        (by epoch) aborts and is rerun, -1 every window -- test hooks).
+        spx_set_chain_handshake."""
         self._check(self._lib.spx_set_chain_handshake(self._ctx, int(us)),
                     "spx_set_chain_handshake")
 

@@ -73,8 +73,8 @@ def _full_solve(name, window=24, chain=0):
     return fx
 
 
-@pytest.mark.parametrize("window,chain,lean", [(24, 0, 0), (28, 0, 0), (24, 0, 1)],
-                         ids=["k24", "k28", "k24-lean"])
+@pytest.mark.parametrize("window,chain,lean", [(24, 0, 0), (28, 0, 0), (24, 0, 1), (24, 0, 2)],
+                         ids=["k24", "k28", "k24-lean", "k24-lean2"])
 def test_config3_dantzig_full_solve_pinned(window, chain, lean, monkeypatch):
     """Config 3 (8192 x 8192 dense LP, tableau 8193 x 16385): the whole
     Dantzig solve at K = 24 and 28 (and with the LEAN chain, SPX_CHAIN_LEAN)

@@ -26,9 +26,10 @@ pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def _peer_threads(world, kind, m, n, seed, rule, K, peer=True, mode=0, **solve_kw):
+def _peer_threads(world, kind, m, n, seed, rule, K, peer=True, mode=0, push=False, **solve_kw):
     """world virtual ranks on GPU 0, each loading its rows and (peer=True)
-    joining the row-sharded persistent chain; returns rank -> results."""
+    joining the row-sharded persistent chain (push: the owner-push row
+    transport); returns rank -> results."""
     from simplex_amd import dist, synth
     uid = bytes([world, m % 251, n % 251, seed % 251, 7]) + os.urandom(123)
     outs, errors = {}, []
@@ -42,7 +43,8 @@ def _peer_threads(world, kind, m, n, seed, rule, K, peer=True, mode=0, **solve_k
                 s.set_chain(mode)
                 s.load_shard(T, obj, basis, m, r0)
                 if peer:
-                    s.enable_peer_chain()
+                    s.enable_peer_chain(push=push)
+                    assert s.peer_push() == int(push)
                 blocks = s.chain_blocks()
                 res = s.solve(rule=rule, **solve_kw)
                 outs[rank] = (r0, r1, res, s.history().tolist(), s.tableau(), s.basis(), blocks,
@@ -93,6 +95,68 @@ def test_peer_chain_virtual_ranks_bit_exact(world, kind, m, n, rule, K):
     assert all(o[6] >= 1 for o in outs.values()), "the persistent sharded chain was not set up"
     assert len({o[7] for o in outs.values()}) == 1, "ranks disagree on the windows rerun"
     _check_vs_oracle(outs, kind, m, n, 3, rule)
+
+
+@pytest.mark.parametrize("world,kind,m,n,rule,K", [
+    (2, "dense", 200, 300, "dantzig", 8),
+    (3, "dense", 301, 257, "dantzig", 24),
+    (3, "dense", 1024, 2048, "dantzig", 16),
+    (2, "degenerate", 64, 64, "bland", 12),
+    (3, "degenerate", 96, 96, "bland", 32),
+    (3, "dense", 7, 9, "dantzig", 4),
+])
+def test_peer_chain_owner_push_bit_exact(world, kind, m, n, rule, K):
+    """The owner-push row transport (spx_set_peer_push: the leaving row's owner
+    writes its stale values into every peer's inbox, halves by pivot parity;
+    no window-end barrier): the oracle's bytes on every rank."""
+    outs = _peer_threads(world, kind, m, n, 3, rule, K, push=True)
+    assert all(o[6] >= 1 for o in outs.values())
+    _check_vs_oracle(outs, kind, m, n, 3, rule)
+
+
+def test_peer_chain_ranks_must_agree_on_the_transport():
+    """Every rank must choose the same row transport: a group whose ranks
+    disagree fails at spx_peer_chain_local on every rank (no rank runs a chain
+    whose peers never push, or never read)."""
+    from simplex_amd import dist, synth
+    from simplex_amd.engine import SpxError
+    m, n, world = 60, 80, 2
+    uid = b"push-agree" + os.urandom(118)
+    errs = {}
+
+    def rank_main(rank):
+        r0, r1 = dist.row_partition(m, world, rank)
+        T, obj, basis = synth.tableau_rows("dense", m, n, 4, r0, r1, order="F")
+        with dist.ShardedTableau(0, rank, world, uid, local=True) as s:
+            s.set_window(8)
+            s.load_shard(T, obj, basis, m, r0)
+            try:
+                s.enable_peer_chain(push=(rank == 1))
+                errs[rank] = None
+            except SpxError as ex:
+                errs[rank] = str(ex)
+
+    th = [threading.Thread(target=rank_main, args=(r,)) for r in range(world)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=120)
+    assert all(errs[r] and "transport" in errs[r] for r in range(world)), errs
+
+
+@pytest.mark.parametrize("world,K", [(2, 24), (3, 24)])
+def test_peer_chain_config3_width_push(world, K):
+    """Config-3 width with the owner-push transport: 64 blocks per rank, each
+    owner block pushing 256 columns; the same bytes as the launch-per-phase
+    sharded path and the pull transport."""
+    kw = dict(max_iters=5 * K + 7)
+    m, n = 400, 15984
+    push = _peer_threads(world, "dense", m, n, 9, "dantzig", K, push=True, **kw)
+    pull = _peer_threads(world, "dense", m, n, 9, "dantzig", K, **kw)
+    assert all(o[6] == 64 for o in push.values())
+    for r in range(world):
+        assert push[r][3] == pull[r][3] and push[r][4].tobytes() == pull[r][4].tobytes()
+    _check_vs_oracle(push, "dense", m, n, 9, "dantzig", max_iters=5 * K + 7)
 
 
 @pytest.mark.parametrize("world,K", [(2, 24), (3, 24), (2, 32)])
@@ -276,11 +340,20 @@ def _free_port():
 @pytest.mark.parametrize("args", [
     ["--rows", "600", "--cols", "900", "--window", "8"],
     ["--rows", "400", "--cols", "15984", "--window", "24", "--pivots", "100"],
+    ["--rows", "400", "--cols", "15984", "--window", "24", "--pivots", "100", "--push"],
     # one context reloaded with LPs of other sizes and then the first again:
-    # the peers re-import buffers that were freed and allocated anew
-    # (the same-device flake)
+    # the peers re-import buffers that were freed and allocated anew, after
+    # every peer released its mapping of them
     ["--rows", "512", "--cols", "2048", "--window", "24", "--pivots", "101",
-     "--then", "1024x8000,512x2048,1024x8000"],
+     "--then", "1024x8000,512x2048,1024x8000", "--ipc-log"],
+    ["--rows", "512", "--cols", "2048", "--window", "24", "--pivots", "101",
+     "--then", "1024x8000,512x2048", "--push"],
+    # peer-only shards have no launch-per-phase path: every 3rd window aborts
+    # at its start handshake and reruns persistent -- 30+ isolated aborts in
+    # one solve, more than the 16 CONSECUTIVE ones a rank gives up after
+    # (the count restarts once the solve moved past the abort)
+    ["--rows", "300", "--cols", "500", "--window", "4", "--pivots", "400",
+     "--abort-every", "3"],
 ])
 def test_peer_chain_two_processes_ipc(args):
     """Two processes on GPU 0, no RCCL: IPC handles of each rank's tableau and
@@ -294,7 +367,13 @@ def test_peer_chain_two_processes_ipc(args):
            *args]
     p = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=280)
     out = p.stdout + p.stderr
+    print(out[-3000:])
     assert p.returncode == 0 and "RCCL_RANKS_CHECK PASS" in out, out[-4000:]
+    if "--abort-every" in args:
+        import re
+        reruns = [int(x) for x in re.search(r"chain reruns per rank \[([^\]]*)\]", out)
+                  .group(1).split(",")]
+        assert min(reruns) > 16, reruns
 
 
 @pytest.mark.timeout(400)
@@ -322,7 +401,11 @@ def test_bench_same_device_two_ranks():
     assert line["n_gpus"] == 2 and line["steps"] == 4
     assert line["config"]["workload"].startswith("config 4")
     assert line["config"]["same_device"] is True
-    assert line["config"]["peer_chain"]["enabled"] is True, line["config"]["peer_chain"]
+    pc = line["config"]["peer_chain"]
+    assert pc["enabled"] is True, pc
+    # both transports passed the self-test; the auto trial timed each and chose one
+    assert pc["push_selftest"] is True and pc["row_transport"] in ("pull", "push"), pc
+    assert set(pc["row_trial_ms_per_window"]) == {"pull", "push"}, pc
     assert line["config"]["chain_blocks"] == 64
     rf = line["roofline"]
     assert rf["kernel"] == "spx::flush_lds_kernel" and 0 < rf["frac"] < 1.0
@@ -332,3 +415,63 @@ def test_bench_same_device_two_ranks():
     assert 5 * 24 <= k <= len(z["hist"])
     want = hashlib.sha256(np.ascontiguousarray(z["hist"][:k], dtype="<i8").tobytes()).hexdigest()
     assert line["pivots_sha256"] == want, "the sharded run's pivots differ from the oracle's"
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("push", [False, True], ids=["pull", "push"])
+def test_peer_chain_eight_processes_config4_240_pinned(push):
+    """Config 4's rank count on one GPU (VERDICT r4 do-this 1): 8 processes,
+    peer-only shards of the config-3 tableau (8 x 1024 rows x 16385 columns),
+    512-thread chain blocks so 8 x 32 = 256 blocks fit the CUs, IPC-mapped
+    peers, 10 windows of 24 pivots.  Every rank's pivot sequence is the
+    oracle's fixture prefix and the assembled tableau's SHA-256 equals the
+    fixture's checkpoint after 240 pivots; the windows rerun after a start
+    handshake abort are printed (chain reruns)."""
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", HSA_ENABLE_IPC_MODE_LEGACY="0")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=8",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.join(ROOT, "tools", "rccl_ranks_check.py"), "--peer", "2", "--same-device",
+           "--rows", "8192", "--cols", "8192", "--seed", "20251205", "--window", "24",
+           "--pivots", "240", "--chain", "3", "--fixture", "config3"] + (["--push"] if push else [])
+    p = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=580)
+    out = p.stdout + p.stderr
+    print(out[-3000:])
+    assert p.returncode == 0 and "RCCL_RANKS_CHECK PASS" in out, out[-4000:]
+    assert "fixture match True" in out and "chain reruns per rank" in out
+
+
+def test_exported_buffer_pool_is_bounded_and_reused():
+    """A row shard's exported tableau and record buffer are never freed
+    before destroy (a new allocation at a freed exported address faulted the
+    peer): reloads park them in a pool, a later load takes the
+    smallest pooled buffer that fits (the same address, so the same IPC
+    handle), and a fifth distinct size fails loudly instead of growing the
+    pool; the context stays usable."""
+    from simplex_amd import dist, synth
+    from simplex_amd.engine import SpxError
+    # tableau sizes in distinct pool classes: 2.6, 10, 41, 165 MB, then 421 MB
+    sizes = [(256, 1000), (512, 2000), (1024, 4000), (2048, 8000), (4096, 8000)]
+    with dist.ShardedTableau(0, 0, 1, local="peer") as s:
+        s.set_window(8)
+        first = None
+        for k, (m, n) in enumerate(sizes):
+            T, obj, basis = synth.tableau_rows("dense", m, n, 5, 0, m, order="F")
+            if k == len(sizes) - 1:
+                with pytest.raises(SpxError, match="pool"):
+                    s.load_shard(T, obj, basis, m, 0)
+                break
+            s.load_shard(T, obj, basis, m, 0)
+            s.enable_peer_chain(allgather=lambda b: [b])
+            if first is None:
+                first = s.peer_debug()
+            s.solve(max_iters=20)
+        m, n = sizes[0]
+        T, obj, basis = synth.tableau_rows("dense", m, n, 5, 0, m, order="F")
+        s.load_shard(T, obj, basis, m, 0)
+        s.enable_peer_chain(allgather=lambda b: [b])
+        again = s.peer_debug()
+        assert (again["A"], again["records"]) == (first["A"], first["records"])
+        res = s.solve()
+        Tf, bf = synth.full_tableau("dense", m, n, 5)
+        st, hist = O.solve_tableau(Tf, bf)
+        assert res.status == st and [tuple(x) for x in s.history().tolist()] == hist

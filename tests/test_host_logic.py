@@ -315,3 +315,15 @@ def test_bench_all_cores_projection_bounds():
     # unknown host model: no roofline, the linear figure bounds it
     b = bench._all_cores_projection(205.0, 16, dict(host, model="other"), bpp, curve)
     assert b["dram_roofline_pivots_per_s"] is None and b["upper_bound"] == 205.0 * 8
+
+
+def test_row_transport_choice_is_deterministic_and_guarded():
+    """bench.py's N > 1 transport trial: every rank passes the same
+    all-reduced times, so every rank takes the same transport; push only when
+    its self-test passed and it was faster (ties stay on pull)."""
+    from simplex_amd.dist import choose_row_transport
+    assert choose_row_transport(10.0, 8.0) == "push"
+    assert choose_row_transport(8.0, 10.0) == "pull"
+    assert choose_row_transport(8.0, 8.0) == "pull"
+    assert choose_row_transport(10.0, 8.0, push_ok=False) == "pull"
+    assert choose_row_transport(10.0, None) == "pull"

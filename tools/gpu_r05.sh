@@ -11,6 +11,10 @@ run() { local lim=$1 log=$2; shift 2
 PYT="python -u -m pytest -x -v --timeout 300 --timeout-method thread"
 for s in ${STEPS:-probe tests bench}; do
   case $s in
+    ipcdiag) # the IPC reload diagnostic: addresses, handles, mapped peers per
+        # load; no pivots run.  IPCENV e.g. "SPX_IPC_ORDER=0" (round 4 order, no keep)
+        TAILN=20 run 240 ipcdiag${PHTAG:-}.log env ${IPCENV:-SPX_IPC_KEEP=0} python -m torch.distributed.run --nnodes=1 --nproc-per-node=2 --master-addr 127.0.0.1 --master-port 29541 tools/rccl_ranks_check.py --peer 2 --same-device --rows 512 --cols 2048 --window 24 --then 1024x8000,512x2048,1024x8000,512x2048 --ipc-log --no-solve ;;
+    same8) TAILN=2 run 500 bench_same8.log python -m torch.distributed.run --nnodes=1 --nproc-per-node=8 --master-addr 127.0.0.1 --master-port 29535 bench.py --gpus 8 --same-device --chain 3 --steps 10 --warmup 2 --cpu-seconds 0 ;;
     strag) TAILN=80 run 300 stragglers${PHTAG:-}.log python tools/probe_stragglers.py --windows ${SWIN:-40} --npz $O/stragglers${PHTAG:-}.npz ${PHARGS:-} ;;
     tests) if [ -n "${KEXPR:-}" ]; then
              run 900 pytest_sel.log $PYT ${TESTS:-tests/test_gpu_chain.py tests/test_gpu_peer_chain.py} -k "$KEXPR"

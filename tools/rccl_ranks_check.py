@@ -16,6 +16,14 @@ would take --m / --n as abbreviations of its own options.)
 --then "R1xC1,R2xC2,...": after the first LP, reload the SAME context with
 each of these LPs in turn (re-export / re-import of the peers, so a rank's
 freed-and-reallocated buffers are mapped again), checking each run.
+--chain M: the persistent chain's mode (3: 512-thread blocks, so 8 ranks' 32
+blocks fit one GPU's 256 CUs with --same-device).  --push: the owner-push row
+transport (spx_set_peer_push).  --fixture NAME: check against the fullsize
+fixture (tests/golden/fullsize.json: the oracle's pivot prefix and the
+assembled tableau's SHA-256 checkpoint after --pivots) instead of running the
+oracle here (config 3 is 1 GB).  --ipc-log: print every rank's exported
+addresses, IPC handle digests and mapped peer pointers per load (DESIGN.md
+§5c); --no-solve skips the pivots (the IPC diagnostic alone).
 """
 import argparse
 import os
@@ -41,6 +49,13 @@ def main():
     ap.add_argument("--seed", type=int, default=17)
     ap.add_argument("--same-device", action="store_true")
     ap.add_argument("--then", default="", help="reload sizes, e.g. 200x2000,600x900")
+    ap.add_argument("--chain", type=int, default=0)
+    ap.add_argument("--push", action="store_true")
+    ap.add_argument("--fixture", default="")
+    ap.add_argument("--ipc-log", action="store_true")
+    ap.add_argument("--no-solve", action="store_true")
+    ap.add_argument("--abort-every", type=int, default=0,
+                    help="force a start-handshake abort of every k-th window (test hook)")
     a = ap.parse_args()
     dist.init_process_group("gloo")
     rank, world = dist.get_rank(), dist.get_world_size()
@@ -54,37 +69,92 @@ def main():
     else:
         s = sdist.ShardedTableau(dev, rank, world, sdist.exchange_unique_id())
     runs = []
+    import hashlib
     with s:
         s.set_window(a.window)
+        s.set_chain(a.chain)
+        if a.abort_every:
+            s.set_chain_handshake(-a.abort_every)
         for rows, cols in sizes:  # one context, reloaded for every LP
             r0, r1 = sdist.row_partition(rows, world, rank)
             T, obj, basis = synth.tableau_rows(a.kind, rows, cols, a.seed, r0, r1, order="F")
             s.load_shard(T, obj, basis, rows, r0)
+            del T
+            blob_digest = None
             if a.peer:
-                s.enable_peer_chain()
+                blobs = []
+
+                def allgather(blob):
+                    out = [None] * world
+                    dist.all_gather_object(out, blob)
+                    blobs.extend(out)
+                    return out
+                s.enable_peer_chain(allgather=allgather, push=a.push)
+                # the IPC handles of every rank's tableau and record buffer
+                blob_digest = [hashlib.sha256(b[16:144]).hexdigest()[:16] for b in blobs]
+            if a.ipc_log:
+                d = s.peer_debug() if a.peer else {}
+                print(f"IPC {rows}x{cols} rank {rank}: A {d.get('A', 0):#x} records "
+                      f"{d.get('records', 0):#x} gen {d.get('gen')} handles {blob_digest} "
+                      f"mapped A {[hex(x) for x in d.get('peer_A', [])]} records "
+                      f"{[hex(x) for x in d.get('peer_records', [])]}", flush=True)
             blocks = s.chain_blocks()
+            if a.no_solve:
+                runs.append(None)
+                continue
             res = s.solve(max_iters=a.pivots, rule=a.rule, use_graph=True)
-            out = (r0, r1, res.status, s.history().tolist(), s.tableau(), s.basis(), blocks)
+            Tl = s.tableau()
+            out = (r0, r1, res.status, s.history().tolist(), Tl if not a.fixture else None,
+                   s.basis(), blocks, s.chain_reruns(), s.peer_push() if a.peer else -1)
             outs = [None] * world
             dist.all_gather_object(outs, out)
-            runs.append(outs)
+            parts = [None] * world if rank == 0 else None
+            if a.fixture:  # the rows go to rank 0 only (1 GB at config 3)
+                dist.gather_object(Tl, parts, dst=0)
+            del Tl
+            runs.append((outs, parts))
     ok = True
-    if rank == 0:
+    if rank == 0 and not a.no_solve:
         from oracle import simplex_oracle as O
-        for (rows, cols), outs in zip(sizes, runs):
-            Tf, bf = synth.full_tableau(a.kind, rows, cols, a.seed)
-            st, hist = O.solve_tableau(Tf, bf, rule=a.rule, max_iters=a.pivots)
-            for q, (r0, r1, stq, h, Tl, b, nb) in enumerate(outs):
-                good = ([tuple(x) for x in h] == hist and np.array_equal(Tl[:-1], Tf[r0:r1])
-                        and np.array_equal(Tl[-1], Tf[-1]) and np.array_equal(b, bf)
-                        and stq == st)
-                print(f"{rows}x{cols} rank {q}: rows {r0}:{r1} status {stq} pivots {len(h)} "
-                      f"chain blocks {nb} bit-exact {good}", flush=True)
-                ok &= good
+        for (rows, cols), (outs, parts) in zip(sizes, runs):
+            print(f"{rows}x{cols}: chain reruns per rank {[o[7] for o in outs]}, row transport "
+                  f"{['push' if o[8] == 1 else 'pull' if o[8] == 0 else '-' for o in outs]}",
+                  flush=True)
+            if a.fixture:
+                import json
+                gold = os.path.join(ROOT, "tests", "golden")
+                fx = json.load(open(os.path.join(gold, "fullsize.json")))[a.fixture]
+                hist = [tuple(x) for x in np.load(os.path.join(
+                    gold, f"fullsize_{a.fixture}.npz"))["hist"][:a.pivots].tolist()]
+                assert (fx["m"], fx["n"], fx["seed"]) == (rows, cols, a.seed), "fixture LP differs"
+                Tall = np.vstack([p_[:-1] for p_ in parts] + [parts[0][-1:]])
+                dig = hashlib.sha256(np.ascontiguousarray(Tall).tobytes()).hexdigest()
+                good_t = dig == fx["checkpoint_sha256"][str(a.pivots)]
+                same_obj = all(np.array_equal(p_[-1], parts[0][-1]) for p_ in parts)
+                print(f"assembled tableau after {a.pivots} pivots: sha256 {dig[:16]} "
+                      f"fixture match {good_t}, objective rows equal {same_obj}", flush=True)
+                ok &= good_t and same_obj
+                for q, (r0, r1, stq, h, _, b, nb, *_r) in enumerate(outs):
+                    good = [tuple(x) for x in h] == hist and stq == 1
+                    print(f"rank {q}: rows {r0}:{r1} status {stq} pivots {len(h)} chain blocks {nb} "
+                          f"pivots = fixture {good}", flush=True)
+                    ok &= good and np.array_equal(b, outs[0][5])
+            else:
+                Tf, bf = synth.full_tableau(a.kind, rows, cols, a.seed)
+                st, hist = O.solve_tableau(Tf, bf, rule=a.rule, max_iters=a.pivots)
+                for q, (r0, r1, stq, h, Tl, b, nb, *_r) in enumerate(outs):
+                    good = ([tuple(x) for x in h] == hist and np.array_equal(Tl[:-1], Tf[r0:r1])
+                            and np.array_equal(Tl[-1], Tf[-1]) and np.array_equal(b, bf)
+                            and stq == st)
+                    print(f"{rows}x{cols} rank {q}: rows {r0}:{r1} status {stq} pivots {len(h)} "
+                          f"chain blocks {nb} bit-exact {good}", flush=True)
+                    ok &= good
             if a.peer:
                 ok &= all(o[6] > 0 for o in outs)  # the persistent chain ran
+                ok &= all(o[8] == (1 if a.push else 0) for o in outs)
         print("RCCL_RANKS_CHECK", "PASS" if ok else "FAIL",
-              f"world={world} peer={a.peer} window={a.window} loads={len(sizes)}", flush=True)
+              f"world={world} peer={a.peer} window={a.window} loads={len(sizes)} "
+              f"push={int(a.push)} chain={a.chain}", flush=True)
     flag = [ok]
     dist.broadcast_object_list(flag, src=0)
     dist.destroy_process_group()
