@@ -147,7 +147,7 @@ struct spx_ctx {
   size_t A_bytes = 0, gr_bytes = 0;
   int chain_mode = 0;      // 0: persistent chain when it fits, 1: launch per phase
   int chain_min_blocks = 0;
-  int chain_lean = 0;      // chain_kernel<.., LEAN> (SPX_CHAIN_LEAN 0..2, A/B hook; spx_chain.hpp)
+  int chain_lean = 1;      // LEAN slot chains (spx_chain.hpp); SPX_CHAIN_LEAN=0: the guarded ones
   // admission of the persistent chain (process-wide block budget per device):
   // blocks this context holds, calls holding them (released by a stream host
   // callback once the call's launches have run), and whether the current call
@@ -920,12 +920,14 @@ int enqueue_window_t(spx_ctx* ctx, int npiv, bool time_flush) {
   if (B > 0) {
     const int cpb = (int)((ctx->N - 1 + B - 1) / B);  // (B * cpb == N-1: xown owns the RHS)
     const int rpb = (int)std::max<int64_t>(1, (ctx->m_local + B - 1) / B);
+    // LEAN slot chains (spx_chain.hpp; the default since round 5, SPX_CHAIN_LEAN=0
+    // selects the guarded chains for A/B runs) on the 256-thread blocks
     auto kern = ctx->sharded ? (cb == 512 ? chain_shard_kernel<KMAX, 512>
                                           : chain_shard_kernel<KMAX, 256>)
                              : (cb == 512 ? chain_kernel<KMAX, 512> : chain_kernel<KMAX, 256>);
     if constexpr (KMAX % 4 == 0)
-      if (!ctx->sharded && cb == 256 && ctx->chain_lean)
-        kern = ctx->chain_lean == 1 ? chain_kernel<KMAX, 256, 1> : chain_kernel<KMAX, 256, 2>;
+      if (cb == 256 && ctx->chain_lean)
+        kern = ctx->sharded ? chain_shard_kernel<KMAX, 256, true> : chain_kernel<KMAX, 256, true>;
     hipLaunchKernelGGL(kern, dim3(B), dim3(cb), 0, ctx->stream, ctx->enter_part, ctx->st,
                        (const Params*)ctx->prm, std::max(NWAVE * ctx->nbn, B),
                        (const double*)ctx->A, ctx->ld, ctx->m_local, ctx->N, ctx->obj, ctx->win,
@@ -1413,9 +1415,8 @@ int spx_create(spx_ctx** out, int device) {
   // tuning hook: SPX_FLUSH_TAIL=x (0..50) overrides the flush's tail share
   if (const char* ft = std::getenv("SPX_FLUSH_TAIL"))
     ctx->flush_tail = std::max(0, std::min(50, std::atoi(ft)));
-  // the single-GPU chain's LEAN slot chains (0 / 1; A/B hook, spx_chain.hpp)
-  if (const char* cl = std::getenv("SPX_CHAIN_LEAN"))
-    ctx->chain_lean = std::max(0, std::min(2, std::atoi(cl)));
+  // the chains' LEAN slot chains (default 1; 0 = the guarded chains, A/B hook)
+  if (const char* cl = std::getenv("SPX_CHAIN_LEAN")) ctx->chain_lean = std::atoi(cl) != 0;
   // windows per replayed graph (1..16; tuning hook)
   if (const char* gw = std::getenv("SPX_GRAPH_WINDOWS"))
     ctx->graph_windows = std::max(1, std::min(16, std::atoi(gw)));

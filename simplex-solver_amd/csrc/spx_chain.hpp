@@ -674,7 +674,7 @@ __device__ __forceinline__ double sys_load(const double* p) {
 // written by the previous kernel (norm<INIT> or the previous window's chain);
 // the chain writes one partial per block there for the next window.
 // ---------------------------------------------------------------------------
-template <int KMAX, int CB, int LEAN = 0>
+template <int KMAX, int CB, bool LEAN = false>
 __global__ __launch_bounds__(CB) void chain_kernel(
     Key* __restrict__ enter_part, State* st, const Params* __restrict__ prm, int n_ep,
     const double* __restrict__ A, int64_t ld, int64_t m, int64_t N, double* __restrict__ obj,
@@ -687,12 +687,9 @@ __global__ __launch_bounds__(CB) void chain_kernel(
   // "s < q" select.  A slot s >= q is an exact identity instead: its f and p
   // histories are +0 (LDS zeroed at the window start, record lanes >= q are
   // +0), and v - (+0 * +0) = v for every v, -0 and NaN included.  Only a
-  // chunk of CH slots is guarded, by a uniform branch.  LEAN >= 2 also runs
-  // the norm phase's zero-p slots (skip rule, zmask) on that fast chain: p is
-  // taken as +0 there, and v - (f * +0) = v for every finite f unless v = -0
-  // (a chain value can only be -0 when the stale value is), so a wave takes
-  // it when no lane has an entered column (cmask), a -0 stale value with a
-  // zero slot, or a non-finite f.
+  // chunk of CH slots is guarded, by a uniform branch.  (Round 5 also tried
+  // the norm phase's zero-p slots on that chain, p taken as +0: slower, 8.77
+  // against 8.52 us per pivot, profiles/r05/ab_chain_lean.jsonl.)
   constexpr int CH = LEAN ? 4 : KMAX % 8 == 0 ? 8 : KMAX % 4 == 0 ? 4 : 2;
   // LH: the window histories f_s[i] (rows) and p_s[j] (columns) live in LDS,
   // slot-major, one column per thread: a phase reads its thread's slots once
@@ -1002,10 +999,6 @@ __global__ __launch_bounds__(CB) void chain_kernel(
 #pragma unroll
       for (int s = 0; s < KMAX; ++s) ps[s] = psl[s][t];
     }
-    if constexpr (LEAN >= 2) {  // zero-p slots as +0 (the records keep psl's values)
-#pragma unroll
-      for (int s = 0; s < KMAX; ++s) ps[s] = ((zmask >> s) & 1u) ? 0.0 : ps[s];
-    }
     double frl = 0.0, ex[2];
     if (!load_extras<1>(gr_ratio, wb, RATIO_HDR + 2, q + 1, RATIO_HDR, rec_tag(W, q, GK_RATIO),
                         frl, ex, st))
@@ -1023,14 +1016,7 @@ __global__ __launch_bounds__(CB) void chain_kernel(
     // see (piv * +0 may be -0); lanes > q are +0 already
     const double frm = LEAN ? (lane < q ? frl : 0.0) : frl;
     if (__ballot(lane < q && slot_r == r) == 0ull) {
-      bool fast = __ballot(jlive && ((zmask | cmask) & qmn) != 0u) == 0ull;
-      if constexpr (LEAN >= 2)
-        fast = fast ||
-               (__ballot(jlive && (cmask & qmn) != 0u) == 0ull &&
-                __ballot(jlive && (zmask & qmn) != 0u &&
-                         __double_as_longlong(v) == (long long)0x8000000000000000ull) == 0ull &&
-                __ballot(lane < q && !__builtin_isfinite(frl)) == 0ull);
-      if (fast) {
+      if (__ballot(jlive && ((zmask | cmask) & qmn) != 0u) == 0ull) {
 #pragma unroll
         for (int c8 = 0; c8 < KMAX; c8 += CH) {
           if (c8 < q) {
@@ -1245,7 +1231,7 @@ __global__ __launch_bounds__(CB) void chain_kernel(
 // its own body: folded into this one it measured ~1 us per pivot slower
 // (register allocation of a 254-VGPR kernel; profiles/r03/ab_chain_*.jsonl).
 // ---------------------------------------------------------------------------
-template <int KMAX, int CB>
+template <int KMAX, int CB, bool LEAN = false>
 __global__ __launch_bounds__(CB) void chain_shard_kernel(
     Key* __restrict__ enter_part, State* st, const Params* __restrict__ prm, int n_ep,
     const double* __restrict__ A, int64_t ld, int64_t m, int64_t N, double* __restrict__ obj,
@@ -1254,12 +1240,15 @@ __global__ __launch_bounds__(CB) void chain_shard_kernel(
     const ChainPeers* __restrict__ pe) {
   static_assert(KMAX <= 32, "slots are lane-indexed and fit the window buffers");
   constexpr int NW = CB / 64;
-  constexpr int CH = KMAX % 8 == 0 ? 8 : KMAX % 4 == 0 ? 4 : 2;
+  // LEAN: chain_kernel's guard-free slot chains (slots s >= q are identities
+  // on +0 histories; only chunks of CH slots are guarded)
+  constexpr int CH = LEAN ? 4 : KMAX % 8 == 0 ? 8 : KMAX % 4 == 0 ? 4 : 2;
   // LH: the window histories f_s[i] (rows) and p_s[j] (columns) live in LDS,
   // slot-major, one column per thread: a phase reads its thread's slots once
   // and appends one, instead of a 2*KMAX-select register update on the path
   // to the record (and the winner's history is published straight from them)
   constexpr bool LH = KMAX * CB * 16 <= 128 * 1024;
+  static_assert(!LEAN || (LH && KMAX % 4 == 0), "LEAN needs the LDS histories");
   __shared__ double fsl[LH ? KMAX : 1][LH ? CB : 1];
   __shared__ double psl[LH ? KMAX : 1][LH ? CB : 1];
   __shared__ double hl33[NW];  // LH: the wave winners' RHS (the ratio record's extra)
@@ -1361,6 +1350,10 @@ __global__ __launch_bounds__(CB) void chain_shard_kernel(
   // entered at slot s (j == c_s), p_s[j] == 0 under the skip rule
   uint32_t rmask = 0u, cmask = 0u, zmask = 0u;
   if (t == 0) lds_pin[b % PIN] = 0.0;
+  if constexpr (LEAN) {  // slots s >= q read +0 histories (written at slot s only)
+#pragma unroll
+    for (int s = 0; s < KMAX; ++s) fsl[s][t] = psl[s][t] = 0.0;
+  }
   if (status0 != ST_RUNNING) {          // grid-uniform: no pivot in this window
     if (leader)
       for (int s = 0; s < npiv; ++s) win.made[s] = 0;  // (the flush counts made slots)
@@ -1470,7 +1463,8 @@ __global__ __launch_bounds__(CB) void chain_shard_kernel(
             for (int u = 0; u < CH; ++u) {
               const int s = c8 + u;
               const double x = msub(fv, fs[s], rdlane(pcl, s));
-              fv = s < q ? x : fv;
+              if constexpr (LEAN) fv = x;  // (s >= q: +0 histories, an identity)
+              else fv = s < q ? x : fv;
             }
           }
         }
@@ -1483,8 +1477,9 @@ __global__ __launch_bounds__(CB) void chain_shard_kernel(
               const int s = c8 + u;
               const double p_s = rdlane(pcl, s);
               double x = msub(fv, fs[s], p_s);
-              x = ((rmask >> s) & 1u) ? p_s : x;
-              fv = s < q ? x : fv;
+              x = ((rmask >> s) & 1u) ? p_s : x;  // (bit s >= q is never set)
+              if constexpr (LEAN) fv = x;
+              else fv = s < q ? x : fv;
             }
           }
         }
@@ -1635,6 +1630,9 @@ __global__ __launch_bounds__(CB) void chain_shard_kernel(
     // p_s[j] == 0 under the skip rule (zmask: the value is kept)
     const uint32_t qmn = (1u << q) - 1u;
     const bool zb = (zmask & qmn) != 0u;
+    // LEAN: lane q holds the pivot element, which slot q of a chunk must not
+    // see (piv * +0 may be -0); lanes > q are +0 already
+    const double frm = LEAN ? (lane < q ? frl : 0.0) : frl;
     if (__ballot(lane < q && slot_r == r) == 0ull) {
       if (__ballot(jlive && ((zmask | cmask) & qmn) != 0u) == 0ull) {
 #pragma unroll
@@ -1643,8 +1641,9 @@ __global__ __launch_bounds__(CB) void chain_shard_kernel(
 #pragma unroll
             for (int u = 0; u < CH; ++u) {
               const int s = c8 + u;
-              const double x = msub(v, rdlane(frl, s), ps[s]);
-              v = s < q ? x : v;
+              const double x = msub(v, rdlane(frm, s), ps[s]);
+              if constexpr (LEAN) v = x;  // (s >= q: +0 histories, an identity)
+              else v = s < q ? x : v;
             }
           }
         }
@@ -1655,10 +1654,11 @@ __global__ __launch_bounds__(CB) void chain_shard_kernel(
 #pragma unroll
             for (int u = 0; u < CH; ++u) {
               const int s = c8 + u;
-              double x = msub(v, rdlane(frl, s), ps[s]);
-              x = ((zmask >> s) & 1u) ? v : x;
+              double x = msub(v, rdlane(frm, s), ps[s]);
+              x = ((zmask >> s) & 1u) ? v : x;  // (bits s >= q are never set)
               x = ((cmask >> s) & 1u) ? 0.0 : x;
-              v = s < q ? x : v;
+              if constexpr (LEAN) v = x;
+              else v = s < q ? x : v;
             }
           }
         }

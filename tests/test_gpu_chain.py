@@ -63,17 +63,16 @@ def test_chain_matches_lazy_chain_and_oracle(eng_cls, K, shape, rule, mode):
     assert np.array_equal(out, ref) and np.array_equal(b, rb)
 
 
-@pytest.mark.parametrize("lean", [1, 2])
+@pytest.mark.parametrize("lean", [0, 1], ids=["guarded", "lean"])
 @pytest.mark.parametrize("K", [4, 8, 24, 28, 32])
 @pytest.mark.parametrize("shape", [(17, 40), (300, 700), (1025, 2051)])
 @pytest.mark.parametrize("rule", ["dantzig", "bland"])
 def test_chain_lean_variant_bit_exact(eng_cls, monkeypatch, K, shape, rule, lean):
-    """The LEAN chains (SPX_CHAIN_LEAN=1: slot chains without per-slot guards,
-    slots past q run as exact identities on +0 histories; =2: also the zero-p
-    slots of the skip rule on that chain, with p as +0) against the
-    launch-per-phase chain and the oracle, with -0.0 entries and exact zeros
-    (the skip rule's masked paths, and -0 stale values that must keep their
-    sign) in the tableau."""
+    """Both slot-chain forms (SPX_CHAIN_LEAN=1, the default since round 5:
+    no per-slot guards, slots past q run as exact identities on +0
+    histories; =0: round 4's guarded chains) against the launch-per-phase
+    chain and the oracle, with -0.0 entries and exact zeros (the skip rule's
+    masked paths) in the tableau."""
     T, basis = _random_tableau(*shape, seed=shape[0] * 13 + K, zero_frac=0.2)
     m = shape[0] - 1
     rng = np.random.default_rng(K)

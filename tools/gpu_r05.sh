@@ -15,11 +15,25 @@ for s in ${STEPS:-probe tests bench}; do
         # load; no pivots run.  IPCENV e.g. "SPX_IPC_ORDER=0" (round 4 order, no keep)
         TAILN=20 run 240 ipcdiag${PHTAG:-}.log env ${IPCENV:-SPX_IPC_KEEP=0} python -m torch.distributed.run --nnodes=1 --nproc-per-node=2 --master-addr 127.0.0.1 --master-port 29541 tools/rccl_ranks_check.py --peer 2 --same-device --rows 512 --cols 2048 --window 24 --then 1024x8000,512x2048,1024x8000,512x2048 --ipc-log --no-solve ;;
     same8) TAILN=2 run 500 bench_same8.log python -m torch.distributed.run --nnodes=1 --nproc-per-node=8 --master-addr 127.0.0.1 --master-port 29535 bench.py --gpus 8 --same-device --chain 3 --steps 10 --warmup 2 --cpu-seconds 0 ;;
+    sameab) # 2 ranks on GPU 0: the row transports (and the slot chains: SAMEVARS label:row:lean)
+        for r in ${ROUNDS:-1 2 3}; do for v in ${SAMEVARS:-pull:pull:1 push:push:1}; do
+          lab=${v%%:*}; rest=${v#*:}; row=${rest%%:*}; ln=${rest#*:}
+          SPX_CHAIN_LEAN=$ln TAILN=0 run 400 sameab_${lab}_r$r.log python -m torch.distributed.run --nnodes=1 --nproc-per-node=2 --master-addr 127.0.0.1 --master-port 2954$r bench.py --gpus 2 --same-device --peer-row $row --steps 40 --warmup 5 --cpu-seconds 0
+          python - "$O/sameab_${lab}_r$r.log" "$lab" "$r" >> $O/sameab.jsonl <<'PY'
+import json, sys
+l = [x for x in open(sys.argv[1]) if x.startswith("{")][-1]
+d = json.loads(l)
+print(json.dumps({"variant": sys.argv[2], "round": int(sys.argv[3]), "value": round(d["value"], 1),
+                  "ms_per_step": round(d["ms_per_step"], 4), "flush_us": round(d["roofline"]["avg_launch_us"], 1),
+                  "chain_us_per_pivot": round(d["chain"]["us_per_pivot"], 3),
+                  "row_transport": d["config"]["peer_chain"].get("row_transport")}))
+PY
+        done; done; cat $O/sameab.jsonl ;;
     strag) TAILN=80 run 300 stragglers${PHTAG:-}.log python tools/probe_stragglers.py --windows ${SWIN:-40} --npz $O/stragglers${PHTAG:-}.npz ${PHARGS:-} ;;
     tests) if [ -n "${KEXPR:-}" ]; then
-             run 900 pytest_sel.log $PYT ${TESTS:-tests/test_gpu_chain.py tests/test_gpu_peer_chain.py} -k "$KEXPR"
+             run 900 pytest_${TTAG:-sel}.log $PYT ${TESTS:-tests/test_gpu_chain.py tests/test_gpu_peer_chain.py} -k "$KEXPR"
            else
-             run 900 pytest_sel.log $PYT ${TESTS:-tests/test_gpu_chain.py tests/test_gpu_peer_chain.py}
+             run 900 pytest_${TTAG:-sel}.log $PYT ${TESTS:-tests/test_gpu_chain.py tests/test_gpu_peer_chain.py}
            fi ;;
     suite) run 1100 pytest_gpu.log $PYT -m gpu tests ;;
     bench) TAILN=1 run 300 bench_driver.log python bench.py --steps 20 --warmup 5 --cpu-seconds 0 ;;
