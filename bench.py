@@ -100,7 +100,7 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=15.0,
                     help="budget of the CPU-baseline sample (0 disables)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles",
-                                                           "traffic_r04.json"))
+                                                           "traffic_r05.json"))
     return ap.parse_args()
 
 
@@ -326,24 +326,28 @@ def peer_selftest(eng, world, rank, K, tdist, torch, same_device=False, chain=0)
     return ok, "ok" if ok else "peer chain differs from the RCCL path: disabled", push_ok and ok
 
 
-def select_row_transport(eng, K, opts, windows, world, tdist, torch, push_ok):
-    """Time `windows` windows with each leaving-row transport (pull, then
-    owner-push; the same pivots either way, they continue the run), max over
-    ranks, and let every rank take the same choice (dist.choose_row_transport).
-    Returns (choice, per-transport ms per window, pivots made)."""
+def select_row_transport(eng, K, opts, windows, world, tdist, torch, push_ok, rounds=2):
+    """Time `windows` windows with each leaving-row transport, alternating
+    pull / push for `rounds` rounds after the bench's warmup (the same pivots
+    either way; they continue the run), max over ranks per trial and the
+    fastest trial per transport, and let every rank take the same choice
+    (dist.choose_row_transport).  Returns (choice, per-transport best ms per
+    window, pivots made)."""
     from simplex_amd.dist import choose_row_transport
     ms, made = {}, 0
-    for mode in (("pull", "push") if push_ok else ("pull",)):
-        eng.enable_peer_chain(push=(mode == "push"))
-        tdist.barrier()
-        eng.sync()
-        t0 = time.perf_counter()
-        eng.run_pivots(windows * K, **opts)
-        eng.sync()
-        t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
-        tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
-        ms[mode] = 1e3 * float(t.item()) / windows
-        made += windows * K
+    modes = ("pull", "push") if push_ok else ("pull",)
+    for _ in range(rounds):
+        for mode in modes:
+            eng.enable_peer_chain(push=(mode == "push"))
+            tdist.barrier()
+            eng.sync()
+            t0 = time.perf_counter()
+            eng.run_pivots(windows * K, **opts)
+            eng.sync()
+            t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
+            tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
+            ms[mode] = min(ms.get(mode, float("inf")), 1e3 * float(t.item()) / windows)
+            made += windows * K
     return choose_row_transport(ms["pull"], ms.get("push"), push_ok), ms, made
 
 
@@ -424,22 +428,27 @@ def main():
     # ranks start their first window together: a shard chain waits at most
     # 100 ms at its start handshake for the other ranks' blocks
     barrier()
+    eng.run_pivots(n_warm, **opts)
+    eng.sync()
     n_trial = 0
     if peer is not None and peer["enabled"]:
         if args.peer_row == "auto":
-            # a few windows with each transport (they count as warmup), then
-            # every rank takes the faster one (the same, from all-reduced times)
-            choice, trial, n_trial = select_row_transport(eng, K, dict(
-                rule=args.rule, skip_zero_cols=not args.dense, use_graph=use_graph, chunk=32),
-                args.row_trial, world, tdist, torch, push_ok)
+            # after the warmup: a few windows with each transport, alternating
+            # (they count as warmup too), then every rank takes the faster one
+            # (the same, from all-reduced times)
+            choice, trial, n_trial = select_row_transport(eng, K, opts, args.row_trial, world,
+                                                          tdist, torch, push_ok)
             peer["row_trial_ms_per_window"] = trial
         else:
             choice = "push" if (args.peer_row == "push" and push_ok) else "pull"
         eng.enable_peer_chain(push=(choice == "push"))
         peer["row_transport"] = choice
+        # the re-import dropped the cached window graphs: rebuild them here,
+        # outside the timed region, with one more window
         barrier()
-    eng.run_pivots(n_warm, **opts)
-    eng.sync()
+        eng.run_pivots(per_step, **opts)
+        eng.sync()
+        n_trial += per_step
     eng.elim_timing(reset=True)
     barrier()
     eng.sync()
