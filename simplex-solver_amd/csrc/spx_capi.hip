@@ -131,6 +131,7 @@ struct spx_ctx {
   std::map<const void*, int> flush_bpc;
   int flush_map = 0;       // flush block -> (row chunk, column group) map
   int flush_tail = FLUSH_TAIL_DEFAULT;  // % of the records rows moved to the tail (spx_delayed.hpp)
+  int flush_tail_r0 = 0;   // 1: the tail to the first dispatch round only (SPX_FLUSH_TAIL_R0)
   int last_flush_G = 0;    // column groups of the last flush launch
   int last_flush_rch = 0;  // row chunks of the last flush launch
   int n_cu = 0;
@@ -985,7 +986,7 @@ int enqueue_window_t(spx_ctx* ctx, int npiv, bool time_flush) {
     ctx->last_flush_rch = rch;
     hipLaunchKernelGGL(kern, dim3(rch * G), dim3(threads), 0, ctx->stream, ctx->A, ctx->ld,
                        ctx->m_local, ctx->row0, ctx->N, ctx->win, npiv, rch, G, ctx->prm,
-                       ctx->st, ctx->flush_map | ctx->flush_tail << 8);
+                       ctx->st, ctx->flush_map | ctx->flush_tail << 8 | ctx->flush_tail_r0 << 16);
   };
   const bool nts = (ctx->elim_nt & 2) != 0;
   // the LDS-DMA ring of 12 columns per wave over the window's compacted
@@ -1415,6 +1416,7 @@ int spx_create(spx_ctx** out, int device) {
   // tuning hook: SPX_FLUSH_TAIL=x (0..50) overrides the flush's tail share
   if (const char* ft = std::getenv("SPX_FLUSH_TAIL"))
     ctx->flush_tail = std::max(0, std::min(50, std::atoi(ft)));
+  if (const char* f0 = std::getenv("SPX_FLUSH_TAIL_R0")) ctx->flush_tail_r0 = std::atoi(f0) != 0;
   // the chains' LEAN slot chains (default 1; 0 = the guarded chains, A/B hook)
   if (const char* cl = std::getenv("SPX_CHAIN_LEAN")) ctx->chain_lean = std::atoi(cl) != 0;
   // windows per replayed graph (1..16; tuning hook)

@@ -29,6 +29,19 @@ print(json.dumps({"variant": sys.argv[2], "round": int(sys.argv[3]), "value": ro
                   "row_transport": d["config"]["peer_chain"].get("row_transport")}))
 PY
         done; done; cat $O/sameab.jsonl ;;
+    tailsweep) # the flush's tail share (SPX_FLUSH_TAIL %, SPX_FLUSH_TAIL_R0): TAILVARS tail:r0 ...
+        for r in ${ROUNDS:-1 2 3}; do for v in ${TAILVARS:-12:0 6:1 9:1 12:1}; do
+          tl=${v%%:*}; t0=${v#*:}
+          SPX_FLUSH_TAIL=$tl SPX_FLUSH_TAIL_R0=$t0 TAILN=0 run 300 tail_${tl}_${t0}_r$r.log python bench.py --steps 40 --warmup 5 --time-every 2 --cpu-seconds 0
+          python - "$O/tail_${tl}_${t0}_r$r.log" "$tl:$t0" "$r" >> $O/tailsweep.jsonl <<'PY'
+import json, sys
+l = [x for x in open(sys.argv[1]) if x.startswith("{")][-1]
+d = json.loads(l)
+print(json.dumps({"variant": sys.argv[2], "round": int(sys.argv[3]), "value": round(d["value"], 1),
+                  "flush_us": round(d["roofline"]["avg_launch_us"], 1), "frac": round(d["roofline"]["frac"], 4),
+                  "chain_us_per_pivot": round(d["chain"]["us_per_pivot"], 3)}))
+PY
+        done; done; cat $O/tailsweep.jsonl ;;
     strag) TAILN=80 run 300 stragglers${PHTAG:-}.log python tools/probe_stragglers.py --windows ${SWIN:-40} --npz $O/stragglers${PHTAG:-}.npz ${PHARGS:-} ;;
     tests) if [ -n "${KEXPR:-}" ]; then
              run 900 pytest_${TTAG:-sel}.log $PYT ${TESTS:-tests/test_gpu_chain.py tests/test_gpu_peer_chain.py} -k "$KEXPR"
@@ -47,9 +60,9 @@ PY
         run 300 $s.log rocprofv3 --kernel-trace --pmc $c -d $O/$s -o p --output-format csv -- python3 bench.py --steps 20 --warmup 5 --cpu-seconds 0 ;;
     ab) # VARIANTS: label=lib:chain[:lean] ... (lib relative to simplex-solver_amd/simplex_amd/lib)
         for r in ${ROUNDS:-1 2 3}; do for v in ${VARIANTS:-base=libspx.so:0:0 lean=libspx.so:0:1}; do
-          lab=${v%%=*}; rest=${v#*=}; lib=${rest%%:*}; rest=${rest#*:}; c=${rest%%:*}; ln=0
-          [ "$rest" != "$c" ] && ln=${rest#*:}
-          SPX_CHAIN_LEAN=$ln SPX_LIB=$PWD/simplex-solver_amd/simplex_amd/lib/$lib SPX_LIB_PARTIAL=1 TAILN=0 \
+          lab=${v%%=*}; rest=${v#*=}; lib=${rest%%:*}; rest=${rest#*:}; c=${rest%%:*}; ln=1; pf=0
+          [ "$rest" != "$c" ] && { rest=${rest#*:}; ln=${rest%%:*}; [ "$rest" != "$ln" ] && pf=${rest#*:}; }
+          SPX_CHAIN_PF=$pf SPX_CHAIN_LEAN=$ln SPX_LIB=$PWD/simplex-solver_amd/simplex_amd/lib/$lib SPX_LIB_PARTIAL=1 TAILN=0 \
             run 300 ab_${lab}_r$r.log python bench.py --chain $c --steps ${ABSTEPS:-40} --warmup 5 --cpu-seconds 0 ${ABARGS:-}
           python - "$O/ab_${lab}_r$r.log" "$lab" "$r" >> $O/ab.jsonl <<'PY'
 import json, sys
