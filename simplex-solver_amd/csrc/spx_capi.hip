@@ -131,7 +131,6 @@ struct spx_ctx {
   std::map<const void*, int> flush_bpc;
   int flush_map = 0;       // flush block -> (row chunk, column group) map
   int flush_tail = FLUSH_TAIL_DEFAULT;  // % of the records rows moved to the tail (spx_delayed.hpp)
-  int flush_tail_r0 = 0;   // 1: the tail to the first dispatch round only (SPX_FLUSH_TAIL_R0)
   int last_flush_G = 0;    // column groups of the last flush launch
   int last_flush_rch = 0;  // row chunks of the last flush launch
   int n_cu = 0;
@@ -148,7 +147,6 @@ struct spx_ctx {
   size_t A_bytes = 0, gr_bytes = 0;
   int chain_mode = 0;      // 0: persistent chain when it fits, 1: launch per phase
   int chain_min_blocks = 0;
-  int chain_lean = 1;      // LEAN slot chains (spx_chain.hpp); SPX_CHAIN_LEAN=0: the guarded ones
   // admission of the persistent chain (process-wide block budget per device):
   // blocks this context holds, calls holding them (released by a stream host
   // callback once the call's launches have run), and whether the current call
@@ -921,14 +919,9 @@ int enqueue_window_t(spx_ctx* ctx, int npiv, bool time_flush) {
   if (B > 0) {
     const int cpb = (int)((ctx->N - 1 + B - 1) / B);  // (B * cpb == N-1: xown owns the RHS)
     const int rpb = (int)std::max<int64_t>(1, (ctx->m_local + B - 1) / B);
-    // LEAN slot chains (spx_chain.hpp; the default since round 5, SPX_CHAIN_LEAN=0
-    // selects the guarded chains for A/B runs) on the 256-thread blocks
     auto kern = ctx->sharded ? (cb == 512 ? chain_shard_kernel<KMAX, 512>
                                           : chain_shard_kernel<KMAX, 256>)
                              : (cb == 512 ? chain_kernel<KMAX, 512> : chain_kernel<KMAX, 256>);
-    if constexpr (KMAX % 4 == 0)
-      if (cb == 256 && ctx->chain_lean)
-        kern = ctx->sharded ? chain_shard_kernel<KMAX, 256, true> : chain_kernel<KMAX, 256, true>;
     hipLaunchKernelGGL(kern, dim3(B), dim3(cb), 0, ctx->stream, ctx->enter_part, ctx->st,
                        (const Params*)ctx->prm, std::max(NWAVE * ctx->nbn, B),
                        (const double*)ctx->A, ctx->ld, ctx->m_local, ctx->N, ctx->obj, ctx->win,
@@ -986,7 +979,7 @@ int enqueue_window_t(spx_ctx* ctx, int npiv, bool time_flush) {
     ctx->last_flush_rch = rch;
     hipLaunchKernelGGL(kern, dim3(rch * G), dim3(threads), 0, ctx->stream, ctx->A, ctx->ld,
                        ctx->m_local, ctx->row0, ctx->N, ctx->win, npiv, rch, G, ctx->prm,
-                       ctx->st, ctx->flush_map | ctx->flush_tail << 8 | ctx->flush_tail_r0 << 16);
+                       ctx->st, ctx->flush_map | ctx->flush_tail << 8);
   };
   const bool nts = (ctx->elim_nt & 2) != 0;
   // the LDS-DMA ring of 12 columns per wave over the window's compacted
@@ -1416,9 +1409,6 @@ int spx_create(spx_ctx** out, int device) {
   // tuning hook: SPX_FLUSH_TAIL=x (0..50) overrides the flush's tail share
   if (const char* ft = std::getenv("SPX_FLUSH_TAIL"))
     ctx->flush_tail = std::max(0, std::min(50, std::atoi(ft)));
-  if (const char* f0 = std::getenv("SPX_FLUSH_TAIL_R0")) ctx->flush_tail_r0 = std::atoi(f0) != 0;
-  // the chains' LEAN slot chains (default 1; 0 = the guarded chains, A/B hook)
-  if (const char* cl = std::getenv("SPX_CHAIN_LEAN")) ctx->chain_lean = std::atoi(cl) != 0;
   // windows per replayed graph (1..16; tuning hook)
   if (const char* gw = std::getenv("SPX_GRAPH_WINDOWS"))
     ctx->graph_windows = std::max(1, std::min(16, std::atoi(gw)));

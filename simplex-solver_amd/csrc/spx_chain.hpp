@@ -674,7 +674,7 @@ __device__ __forceinline__ double sys_load(const double* p) {
 // written by the previous kernel (norm<INIT> or the previous window's chain);
 // the chain writes one partial per block there for the next window.
 // ---------------------------------------------------------------------------
-template <int KMAX, int CB, bool LEAN = false>
+template <int KMAX, int CB>
 __global__ __launch_bounds__(CB) void chain_kernel(
     Key* __restrict__ enter_part, State* st, const Params* __restrict__ prm, int n_ep,
     const double* __restrict__ A, int64_t ld, int64_t m, int64_t N, double* __restrict__ obj,
@@ -683,20 +683,20 @@ __global__ __launch_bounds__(CB) void chain_kernel(
     const ChainPeers* __restrict__ /*pe: shards only*/) {
   static_assert(KMAX <= 32, "slots are lane-indexed and fit the window buffers");
   constexpr int NW = CB / 64;
-  // LEAN (round 5): the slot chains carry no per-slot
-  // "s < q" select.  A slot s >= q is an exact identity instead: its f and p
+  // LEAN (round 5; wherever the LDS histories allow it):
+  // the slot chains carry no per-slot "s < q" select.  A slot s >= q is an exact identity instead: its f and p
   // histories are +0 (LDS zeroed at the window start, record lanes >= q are
   // +0), and v - (+0 * +0) = v for every v, -0 and NaN included.  Only a
   // chunk of CH slots is guarded, by a uniform branch.  (Round 5 also tried
   // the norm phase's zero-p slots on that chain, p taken as +0: slower, 8.77
   // against 8.52 us per pivot, profiles/r05/ab_chain_lean.jsonl.)
-  constexpr int CH = LEAN ? 4 : KMAX % 8 == 0 ? 8 : KMAX % 4 == 0 ? 4 : 2;
   // LH: the window histories f_s[i] (rows) and p_s[j] (columns) live in LDS,
   // slot-major, one column per thread: a phase reads its thread's slots once
   // and appends one, instead of a 2*KMAX-select register update on the path
   // to the record (and the winner's history is published straight from them)
   constexpr bool LH = KMAX * CB * 16 <= 128 * 1024;
-  static_assert(!LEAN || (LH && KMAX % 4 == 0), "LEAN needs the LDS histories");
+  constexpr bool LEAN = LH && KMAX % 4 == 0;
+  constexpr int CH = LEAN ? 4 : KMAX % 8 == 0 ? 8 : KMAX % 4 == 0 ? 4 : 2;
   __shared__ double fsl[LH ? KMAX : 1][LH ? CB : 1];
   __shared__ double psl[LH ? KMAX : 1][LH ? CB : 1];
   __shared__ double hl33[NW];  // LH: the wave winners' RHS (the ratio record's extra)
@@ -1231,7 +1231,7 @@ __global__ __launch_bounds__(CB) void chain_kernel(
 // its own body: folded into this one it measured ~1 us per pivot slower
 // (register allocation of a 254-VGPR kernel; profiles/r03/ab_chain_*.jsonl).
 // ---------------------------------------------------------------------------
-template <int KMAX, int CB, bool LEAN = false>
+template <int KMAX, int CB>
 __global__ __launch_bounds__(CB) void chain_shard_kernel(
     Key* __restrict__ enter_part, State* st, const Params* __restrict__ prm, int n_ep,
     const double* __restrict__ A, int64_t ld, int64_t m, int64_t N, double* __restrict__ obj,
@@ -1240,15 +1240,16 @@ __global__ __launch_bounds__(CB) void chain_shard_kernel(
     const ChainPeers* __restrict__ pe) {
   static_assert(KMAX <= 32, "slots are lane-indexed and fit the window buffers");
   constexpr int NW = CB / 64;
-  // LEAN: chain_kernel's guard-free slot chains (slots s >= q are identities
-  // on +0 histories; only chunks of CH slots are guarded)
-  constexpr int CH = LEAN ? 4 : KMAX % 8 == 0 ? 8 : KMAX % 4 == 0 ? 4 : 2;
+
   // LH: the window histories f_s[i] (rows) and p_s[j] (columns) live in LDS,
   // slot-major, one column per thread: a phase reads its thread's slots once
   // and appends one, instead of a 2*KMAX-select register update on the path
   // to the record (and the winner's history is published straight from them)
   constexpr bool LH = KMAX * CB * 16 <= 128 * 1024;
-  static_assert(!LEAN || (LH && KMAX % 4 == 0), "LEAN needs the LDS histories");
+  // LEAN: chain_kernel's guard-free slot chains (slots s >= q are identities
+  // on +0 histories; only chunks of CH slots are guarded)
+  constexpr bool LEAN = LH && KMAX % 4 == 0;
+  constexpr int CH = LEAN ? 4 : KMAX % 8 == 0 ? 8 : KMAX % 4 == 0 ? 4 : 2;
   __shared__ double fsl[LH ? KMAX : 1][LH ? CB : 1];
   __shared__ double psl[LH ? KMAX : 1][LH ? CB : 1];
   __shared__ double hl33[NW];  // LH: the wave winners' RHS (the ratio record's extra)

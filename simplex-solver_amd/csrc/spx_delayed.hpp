@@ -649,8 +649,9 @@ __device__ __forceinline__ void wait_vmcnt() {
 // (profiles/r02/phases_flush_prio.log).  With a tail share x % (fmap bits
 // 8-15), the last x % of the record rows go to the first two rounds' groups
 // only, still strided: group g takes rows 0..M-1 as before, then (g < Gt =
-// 2G/3) records M*G + g, M*G + g + Gt, ...  (fmap bit 16: Gt = G/3, the first
-// round only; a tuning hook, SPX_FLUSH_TAIL_R0)
+// 2G/3) records M*G + g, M*G + g + Gt, ...  (Round 5: the tail to the first
+// round's groups only was slower at every share, 6-16 %:
+// profiles/r05/flush_tail_first_round_sweep.jsonl.)
 constexpr int FLUSH_TAIL_DEFAULT = 12;  // profiles/r02/ab/flush_tail_split_ab.jsonl
 
 template <int K, int D, bool NTS, bool PART = false>
@@ -687,8 +688,7 @@ __global__ __launch_bounds__(BLK) void flush_lds_kernel(double* __restrict__ A, 
   const int64_t wrow = (int64_t)chunk * 2 * BLK + (int64_t)w * 128;  // this wave's first row
   // this wave's records: g, g+G, ... for rows k < M, then the tail (see above)
   const int tailp = (fmap & 3) == 0 ? (fmap >> 8) & 0xff : 0;
-  // (fmap bit 16: the tail to the first round's groups only, Gt = G / 3)
-  const int Gt = tailp ? max(1, ((fmap >> 16) & 1) ? G / 3 : 2 * G / 3) : G;
+  const int Gt = tailp ? max(1, 2 * G / 3) : G;
   const int M = tailp ? (int)((int64_t)(L / G) * (100 - tailp) / 100) : 0x7fffffff;
   int cnt = g < L ? (L - g + G - 1) / G : 0;
   if (tailp) {

@@ -63,16 +63,16 @@ def test_chain_matches_lazy_chain_and_oracle(eng_cls, K, shape, rule, mode):
     assert np.array_equal(out, ref) and np.array_equal(b, rb)
 
 
-@pytest.mark.parametrize("lean", [0, 1], ids=["guarded", "lean"])
-@pytest.mark.parametrize("K", [4, 8, 24, 28, 32])
+@pytest.mark.parametrize("mode", [2, 3], ids=["cb256", "cb512"])
+@pytest.mark.parametrize("K", [2, 4, 8, 16, 24, 28, 32])
 @pytest.mark.parametrize("shape", [(17, 40), (300, 700), (1025, 2051)])
 @pytest.mark.parametrize("rule", ["dantzig", "bland"])
-def test_chain_lean_variant_bit_exact(eng_cls, monkeypatch, K, shape, rule, lean):
-    """Both slot-chain forms (SPX_CHAIN_LEAN=1, the default since round 5:
-    no per-slot guards, slots past q run as exact identities on +0
-    histories; =0: round 4's guarded chains) against the launch-per-phase
-    chain and the oracle, with -0.0 entries and exact zeros (the skip rule's
-    masked paths) in the tableau."""
+def test_chain_lean_slot_chains_with_negative_zeros_bit_exact(eng_cls, K, shape, rule, mode):
+    """The LEAN slot chains (round 5: no per-slot guards, slots past q run as
+    exact identities on +0 histories; used wherever the LDS histories fit and
+    K % 4 == 0, the guarded chains otherwise: K = 2, and 512-thread blocks
+    with K > 16) against the launch-per-phase chain and the oracle, with -0.0
+    entries and exact zeros (the skip rule's masked paths) in the tableau."""
     T, basis = _random_tableau(*shape, seed=shape[0] * 13 + K, zero_frac=0.2)
     m = shape[0] - 1
     rng = np.random.default_rng(K)
@@ -80,8 +80,7 @@ def test_chain_lean_variant_bit_exact(eng_cls, monkeypatch, K, shape, rule, lean
     T[:m, :T.shape[1] - 1 - m][neg] = -0.0
     kw = dict(max_iters=3 * K + 5, rule=rule)
     res1, h1, out1, b1, _ = _run(eng_cls, T, basis, K, 1, **kw)
-    monkeypatch.setenv("SPX_CHAIN_LEAN", str(lean))
-    res, h, out, b, blocks = _run(eng_cls, T, basis, K, 2, **kw)
+    res, h, out, b, blocks = _run(eng_cls, T, basis, K, mode, **kw)
     assert blocks >= 1
     assert h == h1 and res.status == res1.status and out.tobytes() == out1.tobytes()
     ref, rb = T.copy(), basis.copy()

@@ -73,14 +73,11 @@ def _full_solve(name, window=24, chain=0):
     return fx
 
 
-@pytest.mark.parametrize("window,chain,lean", [(24, 0, 1), (28, 0, 1), (24, 0, 0)],
-                         ids=["k24", "k28", "k24-guarded"])
-def test_config3_dantzig_full_solve_pinned(window, chain, lean, monkeypatch):
+@pytest.mark.parametrize("window,chain", [(24, 0), (28, 0)], ids=["k24", "k28"])
+def test_config3_dantzig_full_solve_pinned(window, chain):
     """Config 3 (8192 x 8192 dense LP, tableau 8193 x 16385): the whole
-    Dantzig solve at K = 24 and 28 (the LEAN slot chains, the default) and
-    with round 4's guarded chains (SPX_CHAIN_LEAN=0) vs the oracle's, index
-    for index."""
-    monkeypatch.setenv("SPX_CHAIN_LEAN", str(lean))
+    Dantzig solve at K = 24 and 28 (the LEAN slot chains) vs the oracle's,
+    index for index."""
     _full_solve("config3", window=window, chain=chain)
 
 

@@ -114,15 +114,6 @@ def test_peer_chain_owner_push_bit_exact(world, kind, m, n, rule, K):
     _check_vs_oracle(outs, kind, m, n, 3, rule)
 
 
-@pytest.mark.parametrize("push", [False, True], ids=["pull", "push"])
-def test_peer_chain_guarded_slot_chains(monkeypatch, push):
-    """The shard chain's round-4 guarded slot chains (SPX_CHAIN_LEAN=0; the
-    LEAN chains are the default) stay bit-exact, with either transport."""
-    monkeypatch.setenv("SPX_CHAIN_LEAN", "0")
-    outs = _peer_threads(3, "dense", 301, 257, 3, "dantzig", 24, push=push)
-    _check_vs_oracle(outs, "dense", 301, 257, 3, "dantzig")
-
-
 def test_peer_chain_ranks_must_agree_on_the_transport():
     """Every rank must choose the same row transport: a group whose ranks
     disagree fails at spx_peer_chain_local on every rank (no rank runs a chain

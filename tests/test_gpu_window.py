@@ -361,19 +361,15 @@ def test_two_phase_driver_auto_window_matches_single_pivot():
 @pytest.mark.parametrize("tail", ["0", "10", "30", "50"])
 @pytest.mark.parametrize("K", [8, 24])
 @pytest.mark.parametrize("shape", [(17, 40), (700, 1500), (1537, 2600)])
-@pytest.mark.parametrize("r0", ["0", "1"])
-def test_window_flush_tail_split_bit_exact(eng_cls, monkeypatch, tail, K, shape, r0):
+def test_window_flush_tail_split_bit_exact(eng_cls, monkeypatch, tail, K, shape):
     """The flush's record split with a tail share (SPX_FLUSH_TAIL, read at
     context creation: the last x % of the record rows go to the first two
-    dispatch rounds' groups, or with SPX_FLUSH_TAIL_R0=1 to the first round's
-    only).  Only which wave updates a column changes, so the bytes are the
-    single-pivot path's."""
+    dispatch rounds' groups).  Only which wave updates a column changes, so the
+    bytes are the single-pivot path's."""
     T, basis = _random_tableau(*shape, seed=shape[0] + 5 * shape[1] + K)
     monkeypatch.setenv("SPX_FLUSH_TAIL", tail)
-    monkeypatch.setenv("SPX_FLUSH_TAIL_R0", r0)
     res, h, out, b = _run(eng_cls, T, basis, K, max_iters=3 * K + 5)
     monkeypatch.delenv("SPX_FLUSH_TAIL")
-    monkeypatch.delenv("SPX_FLUSH_TAIL_R0")
     res0, h0, out0, b0 = _run(eng_cls, T, basis, 0, max_iters=3 * K + 5)
     assert h == h0 and res.status == res0.status and res.iters == res0.iters
     assert out.tobytes() == out0.tobytes() and np.array_equal(b, b0)

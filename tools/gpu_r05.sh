@@ -32,7 +32,7 @@ PY
     tailsweep) # the flush's tail share (SPX_FLUSH_TAIL %, SPX_FLUSH_TAIL_R0): TAILVARS tail:r0 ...
         for r in ${ROUNDS:-1 2 3}; do for v in ${TAILVARS:-12:0 6:1 9:1 12:1}; do
           tl=${v%%:*}; t0=${v#*:}
-          SPX_FLUSH_TAIL=$tl SPX_FLUSH_TAIL_R0=$t0 TAILN=0 run 300 tail_${tl}_${t0}_r$r.log python bench.py --steps 40 --warmup 5 --time-every 2 --cpu-seconds 0
+          SPX_FLUSH_TAIL=$tl TAILN=0 run 300 tail_${tl}_${t0}_r$r.log python bench.py --steps 40 --warmup 5 --time-every 2 --cpu-seconds 0
           python - "$O/tail_${tl}_${t0}_r$r.log" "$tl:$t0" "$r" >> $O/tailsweep.jsonl <<'PY'
 import json, sys
 l = [x for x in open(sys.argv[1]) if x.startswith("{")][-1]
