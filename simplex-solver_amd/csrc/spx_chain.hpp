@@ -581,15 +581,6 @@ __device__ __forceinline__ void publish_record(Dst dst, int nd, unsigned tag, in
 // shard form's destination loop and stop bit, compiled out for one
 // destination, still measured 0.1-0.3 us per pivot slower inside chain_kernel:
 // profiles/r03/ab_chain_regression_bisect.jsonl.)
-// L2: the one-XCD chain (chain_xcd_kernel): every reader shares this XCD's
-// L2, so the granules are plain (workgroup-scope atomic, not write-through)
-// stores that stay in the L2 the readers' sc1 loads are served from.
-template <bool L2>
-__device__ __forceinline__ void g_store_l(gu64* g, unsigned tag, unsigned val) {
-  __hip_atomic_store(g, ((unsigned long long)tag << 32) | val, __ATOMIC_RELAXED,
-                     L2 ? __HIP_MEMORY_SCOPE_WORKGROUP : __HIP_MEMORY_SCOPE_AGENT);
-}
-
 // (pq: the slot, for the probe build's stamps inside the publish; blockIdx 0)
 #if defined(SPX_PHASE_TIMING) && defined(SPX_PROBE_FINE)
 #define SPX_PROBE_PUB(pq, ph, cond) SPX_PROBE((pq) + 32, RATIO ? 0 : 1, ph, cond)
@@ -598,7 +589,7 @@ __device__ __forceinline__ void g_store_l(gu64* g, unsigned tag, unsigned val) {
   do {                              \
   } while (0)
 #endif
-template <int NW, bool RATIO, bool L2 = false, typename Hist>
+template <int NW, bool RATIO, typename Hist>
 __device__ __forceinline__ void publish_local(gu64* rec, int b, unsigned tag, int nh,
                                               const KeyP (&sk)[NW], Hist hist, int pq = 0,
                                               bool mono = false) {
@@ -636,23 +627,23 @@ __device__ __forceinline__ void publish_local(gu64* rec, int b, unsigned tag, in
       const unsigned long long x =
           (unsigned long long)__double_as_longlong(hist(ww, k.row, lane >> 1));
       SPX_PROBE_PUB(pq, 1, x != 12345ull);  // history read from LDS
-      g_store_l<L2>(rb + (size_t)(H0 + lane) * CHAIN_MAX_BLOCKS, tag,
+      g_store(rb + (size_t)(H0 + lane) * CHAIN_MAX_BLOCKS, tag,
                     (lane & 1) ? (unsigned)(x >> 32) : (unsigned)x);
     }
     if (RATIO && lane >= 62) {
       const unsigned long long x =
           (unsigned long long)__double_as_longlong(hist(ww, k.row, 33));
-      g_store_l<L2>(rb + (size_t)(RATIO_HDR + (lane - 62)) * CHAIN_MAX_BLOCKS, tag,
+      g_store(rb + (size_t)(RATIO_HDR + (lane - 62)) * CHAIN_MAX_BLOCKS, tag,
                     (lane & 1) ? (unsigned)(x >> 32) : (unsigned)x);
     }
   }
   if (lane == 0) {
     const unsigned long long vb = (unsigned long long)__double_as_longlong(RATIO ? k.v : k.a);
-    g_store_l<L2>(rb + 0 * CHAIN_MAX_BLOCKS, tag, (unsigned)vb);
-    g_store_l<L2>(rb + 1 * CHAIN_MAX_BLOCKS, tag, (unsigned)(vb >> 32));
-    g_store_l<L2>(rb + 2 * CHAIN_MAX_BLOCKS, tag, none ? 0xffffffffu : (unsigned)k.row);
+    g_store(rb + 0 * CHAIN_MAX_BLOCKS, tag, (unsigned)vb);
+    g_store(rb + 1 * CHAIN_MAX_BLOCKS, tag, (unsigned)(vb >> 32));
+    g_store(rb + 2 * CHAIN_MAX_BLOCKS, tag, none ? 0xffffffffu : (unsigned)k.row);
     if (RATIO)
-      g_store_l<L2>(rb + 3 * CHAIN_MAX_BLOCKS, tag, none ? 0xffffffffu : (unsigned)k.t);
+      g_store(rb + 3 * CHAIN_MAX_BLOCKS, tag, none ? 0xffffffffu : (unsigned)k.t);
   }
   SPX_PROBE_PUB(pq, 2, true);  // every store issued
 }
