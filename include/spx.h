@@ -205,9 +205,13 @@ int spx_pivot_at(spx_ctx* ctx, int64_t r, int64_t c);
  * (spx_sync, spx_state, a getter, or the next call), so the request still
  * ends after exactly `npivots` pivots.  Two duties follow from not waiting:
  * (1) peer-only row shards (spx_create_sharded_peer) must reach that drain
- * together -- the rerun is again a cross-rank persistent chain, and a rank
- * draining much later than its peers (beyond the ~4 s spin bound) leaves
- * them in ST_FAULT; bench.py and dist.py drain every rank right after the
+ * together -- the rerun is again a cross-rank persistent chain.  A rank that
+ * drains late is waited for: the early ranks' rerun windows abort at the
+ * handshake (100 ms each) and are rerun until it arrives, which the late
+ * rank catches up with at once (tested with a 0.6 s lag on one GPU).  Past
+ * 16 consecutive aborts (~1.7 s) the early ranks give up with SPX_E_STATE;
+ * ranks on different GPUs end in ST_FAULT after the ~4 s wait for the other
+ * GPUs' verdicts.  bench.py and dist.py drain every rank right after the
  * call, behind a barrier.  (2) The call's persistent-chain admission
  * (spx_set_chain_budget) is held until that drain, or until another call or
  * admission decision of this process sees the call's work complete; a

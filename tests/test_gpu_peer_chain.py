@@ -12,6 +12,7 @@ process, plain device pointers) and two processes exchanging IPC handles over
 gloo (spx_create_sharded_peer: no RCCL, which refuses two ranks on one GPU).
 """
 import os
+import re
 import socket
 import subprocess
 import sys
@@ -354,6 +355,11 @@ def _free_port():
     # (the count restarts once the solve moved past the abort)
     ["--rows", "300", "--cols", "500", "--window", "4", "--pivots", "400",
      "--abort-every", "3"],
+    # the same through spx_run_pivots: the aborted windows are rerun at the
+    # drain points, and the last rank drains 0.6 s after the first (ADVICE r4:
+    # rp_recover with staggered drains; spx.h spx_run_pivots)
+    ["--rows", "300", "--cols", "500", "--window", "4", "--pivots", "400",
+     "--abort-every", "3", "--run-pivots", "--late-drain", "0.6"],
 ])
 def test_peer_chain_two_processes_ipc(args):
     """Two processes on GPU 0, no RCCL: IPC handles of each rank's tableau and
@@ -370,10 +376,14 @@ def test_peer_chain_two_processes_ipc(args):
     print(out[-3000:])
     assert p.returncode == 0 and "RCCL_RANKS_CHECK PASS" in out, out[-4000:]
     if "--abort-every" in args:
-        import re
         reruns = [int(x) for x in re.search(r"chain reruns per rank \[([^\]]*)\]", out)
                   .group(1).split(",")]
         assert min(reruns) > 16, reruns
+    if "--late-drain" in args:
+        # rank 0's drain waited for the late rank's chain (its rerun windows
+        # aborted at the handshake until rank 1 arrived), then both finished
+        drains = {int(k): float(v) for k, v in re.findall(r"rank (\d+): drain ([0-9.]+) s", out)}
+        assert drains[0] > 0.3 and drains[1] < drains[0], drains
 
 
 @pytest.mark.timeout(400)

@@ -24,6 +24,10 @@ assembled tableau's SHA-256 checkpoint after --pivots) instead of running the
 oracle here (config 3 is 1 GB).  --ipc-log: print every rank's exported
 addresses, IPC handle digests and mapped peer pointers per load (DESIGN.md
 §5c); --no-solve skips the pivots (the IPC diagnostic alone).
+--run-pivots: enqueue the pivots with spx_run_pivots (no host wait) and drain
+with spx_sync, instead of spx_solve; --late-drain S: the last rank sleeps S
+seconds before its drain (a window aborted at its start handshake is rerun at
+the drain points, which then happen S seconds apart: ADVICE r4, spx.h).
 """
 import argparse
 import os
@@ -56,6 +60,8 @@ def main():
     ap.add_argument("--no-solve", action="store_true")
     ap.add_argument("--abort-every", type=int, default=0,
                     help="force a start-handshake abort of every k-th window (test hook)")
+    ap.add_argument("--run-pivots", action="store_true")
+    ap.add_argument("--late-drain", type=float, default=0.0)
     a = ap.parse_args()
     dist.init_process_group("gloo")
     rank, world = dist.get_rank(), dist.get_world_size()
@@ -102,9 +108,23 @@ def main():
             if a.no_solve:
                 runs.append(None)
                 continue
-            res = s.solve(max_iters=a.pivots, rule=a.rule, use_graph=True)
+            if a.run_pivots:
+                import time
+                from simplex_amd import _lib as L
+                s.run_pivots(a.pivots, rule=a.rule, use_graph=True)
+                if a.late_drain and rank == world - 1:
+                    time.sleep(a.late_drain)
+                t0 = time.perf_counter()
+                s.sync()
+                drain_s = time.perf_counter() - t0
+                stq = s.state()[0]
+                stq = 1 if stq == L.SPX_RUNNING else stq  # (the request's end = the oracle's limit)
+                print(f"rank {rank}: drain {drain_s:.3f} s, chain reruns {s.chain_reruns()}",
+                      flush=True)
+            else:
+                stq = s.solve(max_iters=a.pivots, rule=a.rule, use_graph=True).status
             Tl = s.tableau()
-            out = (r0, r1, res.status, s.history().tolist(), Tl if not a.fixture else None,
+            out = (r0, r1, stq, s.history().tolist(), Tl if not a.fixture else None,
                    s.basis(), blocks, s.chain_reruns(), s.peer_push() if a.peer else -1)
             outs = [None] * world
             dist.all_gather_object(outs, out)
