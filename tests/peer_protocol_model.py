@@ -124,6 +124,31 @@ def _wait(pred, what, limit=None):
         time.sleep(POLL_SLEEP)
 
 
+def _wait_all(get, keys, ok, what, limit=None):
+    """Poll until one pass sees ok(get(k)) for every key, and return that
+    pass's values (as the kernels' polls do).  Slots seen matching are not
+    re-read on every pass while the others are awaited -- only the final pass
+    re-reads them all -- so a wait costs about one pass over the slots, not one
+    per poll: with 512 polling block threads (config 4) the full re-read of
+    every pass starved the threads that do the work."""
+    keys = list(keys)
+    nxt = 0
+
+    def pred():
+        nonlocal nxt
+        while nxt < len(keys) and ok(get(keys[nxt])):
+            nxt += 1
+        if nxt < len(keys):
+            return None
+        vals = [get(k) for k in keys]
+        for x, v in enumerate(vals):
+            if not ok(v):
+                nxt = x
+                return None
+        return vals
+    return _wait(pred, what, limit)
+
+
 def _argmin(keys):
     """Lexicographic winner of (value, tie, payload...) tuples (None: no key)."""
     keys = [k for k in keys if k is not None]
@@ -222,8 +247,11 @@ class Rank:
         dev.arrive[slot] = _tag(W, 0, START)
         t0 = time.monotonic()
         want = GO
+        nxt, n = 0, dev.nr * dev.B  # (arrivals seen are not re-read: see _wait_all)
         while True:
-            if all(dev.arrive.get(x) == _tag(W, 0, START) for x in range(dev.nr * dev.B)):
+            while nxt < n and dev.arrive.get(nxt) == _tag(W, 0, START):
+                nxt += 1
+            if nxt == n and all(dev.arrive.get(x) == _tag(W, 0, START) for x in range(n)):
                 break
             if time.monotonic() - t0 > self.hs_bound:
                 want = ABORT
@@ -259,10 +287,9 @@ class Rank:
                 c, zc, pc = c0, (self.obj[c0] if c0 >= 0 else 0.0), []
             else:
                 tag = _tag(W, q - 1, ENTER)
-                recs = _wait(lambda: ([dev.enter[rank].get(x) for x in range(B)]
-                                      if all(dev.enter[rank].get(x, (None,))[0] == tag
-                                             for x in range(B)) else None),
-                             f"rank {rank} block {b}: entering records of slot {q - 1}")
+                recs = _wait_all(lambda x: dev.enter[rank].get(x, (None,)), range(B),
+                                 lambda v: v[0] == tag,
+                                 f"rank {rank} block {b}: entering records of slot {q - 1}")
                 win = _argmin([r[1] for r in recs])
                 c, zc, pc = (win[2], win[3], win[4]) if win else (-1, 0.0, [])
             if c < 0:
@@ -297,10 +324,9 @@ class Rank:
             # ---- norm phase q: leaving row, p on my columns, entering key ----
             self.delay("poll_ratio", rank, b, q)
             tag = _tag(W, q, RATIO)
-            recs = _wait(lambda: ([dev.ratio[rank][h].get(x) for x in dev.slots]
-                                  if all(dev.ratio[rank][h].get(x, (None,))[0] == tag
-                                         for x in dev.slots) else None),
-                         f"rank {rank} block {b}: ratio records of slot {q}")
+            recs = _wait_all(lambda x: dev.ratio[rank][h].get(x, (None,)), dev.slots,
+                             lambda v: v[0] == tag,
+                             f"rank {rank} block {b}: ratio records of slot {q}")
             if any(r[1][1] for r in recs):  # rank 0's stop request, seen by every rank here
                 with lock:
                     sh["status"] = 1
@@ -328,10 +354,9 @@ class Rank:
             if dev.push and owner != rank:
                 tag_r = _tag(W, q, RATIO)
                 box = dev.inbox[rank][h]
-                row = _wait(lambda: ({j: box[j][1] for j in cols}
-                                     if all(box.get(j, (None,))[0] == tag_r for j in cols)
-                                     else None),
-                            f"rank {rank} block {b}: pushed row of slot {q}")
+                got = _wait_all(lambda j: box.get(j, (None,)), cols, lambda v: v[0] == tag_r,
+                                f"rank {rank} block {b}: pushed row of slot {q}")
+                row = {j: v[1] for j, v in zip(cols, got)}
             else:
                 src = dev.A[owner]  # the owner's stale rows (a peer pointer; my own rows)
                 row = {j: src[rl, j] for j in cols}
@@ -369,9 +394,8 @@ class Rank:
             for d in range(nr):
                 dev.done[d][rank * B + b] = _tag(W, 0, DONE)
             if b == 0:
-                _wait(lambda: True if all(dev.done[rank].get(x) == _tag(W, 0, DONE)
-                                          for x in range(nr * B)) else None,
-                      f"rank {rank}: window-end barrier")
+                _wait_all(lambda x: dev.done[rank].get(x), range(nr * B),
+                          lambda v: v == _tag(W, 0, DONE), f"rank {rank}: window-end barrier")
         with lock:
             for j in cols:
                 obj_new[j] = o[j]
