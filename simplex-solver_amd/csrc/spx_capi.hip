@@ -997,7 +997,7 @@ int enqueue_window_t(spx_ctx* ctx, int npiv, bool time_flush) {
   // a tail inside the flush measured 226 vs 182 us
   // (profiles/r03/ab_flush_tail_vs_rowfix.jsonl)
   hipLaunchKernelGGL(row_fix_kernel<KMAX>, dim3(ctx->nbn), dim3(BLK), 0, ctx->stream, ctx->A,
-                       ctx->ld, ctx->m_local, ctx->row0, ctx->N, ctx->win, npiv);
+                     ctx->ld, ctx->m_local, ctx->row0, ctx->N, ctx->win, npiv);
   HIPC(hipGetLastError());
   return SPX_OK;
 }

@@ -365,7 +365,14 @@ __device__ __forceinline__ int chain_start(const gu64* arr, int nslots, int B, u
     bool ok = true;
     for (int x = lane; x < nslots; x += 64)
       if ((gmask >> (x / B)) & 1u) ok &= (unsigned)(g_load<SYS>(arr + x) >> 32) == tag;
+    // (read with the arrivals) the group's verdict word: once it holds W or a
+    // later window, W is decided, so stop waiting.  A rank that reruns late
+    // -- its host drained after its peers' -- then walks through the windows
+    // its peers aborted without waiting out the bound for each, and catches
+    // up with them (tests/test_gpu_peer_chain.py, --late-drain)
+    const unsigned long long vw0 = g_load<SYS>(vword);
     if (__all(ok)) break;
+    if (epoch_diff((uint32_t)(vw0 >> 8), W) >= 0) break;
     late = (int64_t)(__builtin_amdgcn_s_memrealtime() - t0) > bound;
     if (!late && spin_fail(spins, st)) return 2;
   }

@@ -43,6 +43,13 @@ __device__ unsigned long long spx_probe_buf[1024 + 2 * 8192];
     if (threadIdx.x == 0 && blockIdx.x < 8192)                                               \
       spx_probe_buf[1024 + 2 * blockIdx.x + (which)] = __builtin_amdgcn_s_memrealtime();    \
   } while (0)
+// row_fix blocks: [1024 + 2*(4096 + b) + which]
+#define SPX_PROBE_RF_BLOCK(which)                                                            \
+  do {                                                                                       \
+    if (threadIdx.x == 0 && blockIdx.x < 4096)                                               \
+      spx_probe_buf[1024 + 2 * (4096 + blockIdx.x) + (which)] =                              \
+          __builtin_amdgcn_s_memrealtime();                                                  \
+  } while (0)
 #define SPX_PROBE(slot, kind, phase, cond)                                                  \
   do {                                                                                       \
     if (blockIdx.x == 0 && threadIdx.x == 0 && (cond))                                       \
@@ -69,6 +76,9 @@ __device__ unsigned long long spx_probe_wave[2 * 4 * 8192];
   } while (0)
 #define SPX_PROBE_BLOCK(which) \
   do {                         \
+  } while (0)
+#define SPX_PROBE_RF_BLOCK(which) \
+  do {                            \
   } while (0)
 #define SPX_PROBE_WAVE(w, cols) \
   do {                          \
@@ -826,51 +836,89 @@ __global__ __launch_bounds__(BLK) void flush_lds_kernel(double* __restrict__ A, 
 // whose last leaving slot is L ends at p_L[j] followed by the later pivots'
 // msub updates (their leaving rows differ from r).  One thread per column.
 // ---------------------------------------------------------------------------
-template <int K>
-__global__ __launch_bounds__(BLK) void row_fix_kernel(double* __restrict__ A, int64_t ld,
+template <int K, int TPB = BLK>
+__global__ __launch_bounds__(TPB) void row_fix_kernel(double* __restrict__ A, int64_t ld,
                                                       int64_t m_local, int64_t row0, int64_t N,
                                                       Window win, int npiv) {
-  (void)N;
   __shared__ double fr[K][K];  // fr[L][s] = f_s[r_L]
   __shared__ int64_t rows[K];
   __shared__ int lastL[K];
+  __shared__ int made_sh[K];
+  const int t = threadIdx.x;
+  SPX_PROBE(K + 1, 0, 0, true);
+  SPX_PROBE_RF_BLOCK(0);
   // one thread per record of the window (the flush's compacted list: column,
-  // path flags, p_0..p_{K-1}); all loads are independent: issue them together
-  const int kr = blockIdx.x * BLK + threadIdx.x;
-  const bool live = kr < *win.nlist;
-  const int64_t hdr = reinterpret_cast<const int64_t*>(win.rec)[(int64_t)(live ? kr : 0) * RECW];
-  const int64_t j = hdr & 0xffffffffll;
-  const bool fast = (hdr >> 32) == 0;  // not SPECIAL / ZERO: the flush's plain msub chain
-  int madeK = 0;  // made slots of this window: a prefix of its npiv launched ones
-  for (int s = 0; s < npiv; ++s) madeK += win.made[s];
+  // path flags, p_0..p_{K-1}).  Two rounds of dependent loads: (1) the record
+  // (its index clamped to the buffer, not to the list length, so it does not
+  // wait for *nlist), the leaving rows and made flags; (2) the leaving rows' f
+  // histories.  (The first form waited for *nlist before the record and
+  // loaded f_s[r_L] in a loop of dependent r -> F pairs: 15.1 against 13.9 us.
+  // Block-0 stamps, profiles/r05/phases24_rowfix*.log: the kernel starts ~3 us
+  // after the flush's last block, then ~2.7 us of loads, ~4 us of msub chains
+  // and ~2.5 us to issue the scattered stores (the stores themselves: ~1.4
+  // us).  64-thread blocks and the K chains interleaved slot-major measured
+  // 14.3-14.9 us, not kept.)
+  const int kr = blockIdx.x * TPB + t;
+  const int64_t kc = kr < N ? kr : N - 1;  // the record buffer holds N records
+  const int nl = *win.nlist;
+  const int64_t hdr = reinterpret_cast<const int64_t*>(win.rec)[kc * RECW];
   double p[K];
 #pragma unroll
-  for (int s = 0; s < K; ++s) p[s] = win.rec[(int64_t)(live ? kr : 0) * RECW + 2 + s];
-  // (loaded before the made-count check: a slot not made in this window holds a
-  // stale value, so the index is clamped; such values are never used)
-  for (int x = threadIdx.x; x < K * K; x += BLK) {
-    const int L = x / K, s = x % K;
-    const int64_t rl = min(max(win.r[L] - row0, (int64_t)0), m_local - 1);
-    fr[L][s] = win.F[(int64_t)s * ld + rl];
-  }
-  if (threadIdx.x < K) {
-    const int64_t r = win.r[threadIdx.x];
-    bool last = true;  // the last leaving slot of row r among the made ones
-    for (int s = threadIdx.x + 1; s < madeK; ++s) last &= win.r[s] != r;
-    rows[threadIdx.x] = r - row0;
-    lastL[threadIdx.x] = last;
+  for (int s = 0; s < K; ++s) p[s] = win.rec[kc * RECW + 2 + s];
+  if (t < K) {
+    rows[t] = win.r[t] - row0;
+    made_sh[t] = t < npiv ? win.made[t] : 0;
   }
   __syncthreads();
-  if (madeK == 0 || !live || !fast) return;
+  SPX_PROBE(K + 1, 0, 1, hdr != 12345 && p[K - 1] != 12345.678);  // round 1 arrived
+  // made slots of this window: a prefix of its npiv launched ones
+  int madeK = 0;
+#pragma unroll
+  for (int s = 0; s < K; ++s) madeK += made_sh[s];
+  constexpr int PER = (K * K + TPB - 1) / TPB;
+  double fv[PER];
+#pragma unroll
+  for (int u = 0; u < PER; ++u) {
+    const int x = t + u * TPB;
+    fv[u] = 0.0;
+    if (x < K * K) {
+      // (a slot not made in this window holds a stale row: clamped, never used)
+      const int64_t rl = min(max(rows[x / K], (int64_t)0), m_local - 1);
+      fv[u] = win.F[(int64_t)(x % K) * ld + rl];
+    }
+  }
+  if (t < K) {  // the last leaving slot of row r_t among the made ones
+    const int64_t r = rows[t];
+    bool last = true;
+    for (int s = t + 1; s < madeK; ++s) last &= rows[s] != r;
+    lastL[t] = last;
+  }
+#pragma unroll
+  for (int u = 0; u < PER; ++u) {
+    const int x = t + u * TPB;
+    if (x < K * K) fr[x / K][x % K] = fv[u];
+  }
+  SPX_PROBE(K + 1, 0, 2, fv[0] != 12345.678);  // round 2 arrived
+  __syncthreads();
+  SPX_PROBE(K + 1, 1, 2, true);  // lastL and the barrier done
+  const int64_t j = hdr & 0xffffffffll;
+  const bool fast = (hdr >> 32) == 0;  // not SPECIAL / ZERO: the flush's plain msub chain
+  if (madeK == 0 || kr >= nl || !fast) return;
 #pragma unroll
   for (int L = 0; L < K; ++L) {
     if (L >= madeK || !lastL[L] || rows[L] < 0 || rows[L] >= m_local) continue;  // not ours
-    double x = p[L];
+    double x = p[L];  // p_L[j], then the later slots
 #pragma unroll
     for (int s = L + 1; s < K; ++s)
       if (s < madeK) x = msub(x, fr[L][s], p[s]);
     __builtin_nontemporal_store(x, A + j * ld + rows[L]);  // scattered 8-B writes: no L2 allocate
   }
+#ifdef SPX_PHASE_TIMING
+  SPX_PROBE(K + 1, 0, 3, true);  // stores issued
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  SPX_PROBE(K + 1, 1, 0, true);  // stores done
+  SPX_PROBE_RF_BLOCK(1);
+#endif
 }
 
 }  // namespace spx

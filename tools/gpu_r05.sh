@@ -74,6 +74,22 @@ print(json.dumps({"variant": sys.argv[2], "round": int(sys.argv[3]), "value": ro
                   "chain_us_per_pivot": round(d["chain"]["us_per_pivot"], 3)}))
 PY
         done; done; cat $O/ab.jsonl ;;
+    envab) # ENVVARS: label=VAR=value ... (one environment assignment per variant)
+        for r in ${ROUNDS:-1 2 3}; do for v in ${ENVVARS:-t12=SPX_FLUSH_TAIL=12 t10=SPX_FLUSH_TAIL=10}; do
+          lab=${v%%=*}; asg=${v#*=}
+          TAILN=0 run 300 envab_${lab}_r$r.log env $asg python bench.py --steps ${ABSTEPS:-40} --warmup 5 --cpu-seconds 0 ${ABARGS:-}
+          python - "$O/envab_${lab}_r$r.log" "$lab" "$r" >> $O/envab.jsonl <<'PY'
+import json, sys
+l = [x for x in open(sys.argv[1]) if x.startswith("{")][-1]
+d = json.loads(l)
+print(json.dumps({"variant": sys.argv[2], "round": int(sys.argv[3]), "value": round(d["value"], 1),
+                  "ms_per_step": round(d["ms_per_step"], 4), "flush_us": round(d["roofline"]["avg_launch_us"], 1),
+                  "frac": round(d["roofline"]["frac"], 4),
+                  "chain_us_per_pivot": round(d["chain"]["us_per_pivot"], 3)}))
+PY
+        done; done; cat $O/envab.jsonl ;;
+    rpenv) # rocprof kernel stats under one environment assignment (RPENV, RPTAG)
+        run 400 rocprof_${RPTAG:-env}.log env ${RPENV:-SPX_FLUSH_TAIL=12} rocprofv3 --kernel-trace --stats -d $O/prof_${RPTAG:-env} -o bench --output-format csv -- python3 bench.py --steps 20 --warmup 5 --cpu-seconds 0 ;;
     *) echo "unknown step $s"; exit 3 ;;
   esac
 done

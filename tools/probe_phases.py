@@ -128,6 +128,20 @@ def main():
     print("  per-chunk mean dur:", " ".join(f"{x:.0f}" for x in cd))
     xcd = np.arange(nblk) % 8
     print("  per-XCD mean dur:", " ".join(f"{dur[xcd == k].mean():.0f}" for k in range(8)))
+    # row_fix (block 0 stamps, every block's entry / exit) after the flush's last block
+    r0 = us(t(K + 1, 0, 0))
+    if r0 > 0:
+        fl_end = en.max() + f0
+        rb = [(buf[1024 + 2 * (4096 + b)], buf[1024 + 2 * (4096 + b) + 1]) for b in range(4096)]
+        rb = np.array([(us(a_), us(b_)) for a_, b_ in rb if a_ > t0])
+        print(f"row_fix: entry {r0 - fl_end:+6.2f} us after the flush's last block; block 0: "
+              f"round 1 +{us(t(K + 1, 0, 1)) - r0:5.2f}  round 2 +{us(t(K + 1, 0, 2)) - us(t(K + 1, 0, 1)):5.2f}"
+              f"  lastL+barrier +{us(t(K + 1, 1, 2)) - us(t(K + 1, 0, 2)):5.2f}"
+              f"  chains +{us(t(K + 1, 1, 1)) - us(t(K + 1, 1, 2)):5.2f}"
+              f"  store issue +{us(t(K + 1, 0, 3)) - us(t(K + 1, 1, 1)):5.2f}"
+              f"  stores drained +{us(t(K + 1, 1, 0)) - us(t(K + 1, 0, 3)):5.2f}")
+        if len(rb):
+            print(f"  {len(rb)} blocks: entry pct 0/50/100 {q(rb[:, 0] - r0)}  exit pct {q(rb[:, 1] - r0)}")
     if hasattr(lib, "spx_probe_read_wave"):
         wb = (ctypes.c_ulonglong * (2 * 4 * 8192))()
         assert lib.spx_probe_read_wave(wb, 2 * 4 * 8192) == 0
