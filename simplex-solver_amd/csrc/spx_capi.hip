@@ -1775,6 +1775,48 @@ int spx_destroy(spx_ctx* ctx) {
   return SPX_OK;
 }
 
+// Row-major host rows <-> the column-major tableau, in chunks of rows through
+// a device staging buffer (at most ~64 MB, freed after the call): H2D: a 2-D
+// copy of the chunk's rows, then transpose_kernel into A; D2H: the transpose
+// into the staging buffer, then a 2-D copy into the host rows (pitch ld).
+int transfer_rows(spx_ctx* ctx, double* host, int64_t nrows, int64_t cols, int64_t ld,
+                  bool to_device) {
+  const int64_t chunk = std::max<int64_t>(32, std::min<int64_t>(
+                                                  nrows, ((8 << 20) / cols + 31) / 32 * 32));
+  double* stage = nullptr;
+  HIPC(hipMalloc(&stage, sizeof(double) * chunk * cols));
+  int rc = SPX_OK;
+  for (int64_t i0 = 0; i0 < nrows && rc == SPX_OK; i0 += chunk) {
+    const int64_t R = std::min(chunk, nrows - i0);
+    const dim3 grid((unsigned)((cols + 31) / 32), (unsigned)((R + 31) / 32));
+    hipError_t e;
+    if (to_device) {
+      e = hipMemcpy2DAsync(stage, sizeof(double) * cols, host + i0 * ld, sizeof(double) * ld,
+                           sizeof(double) * cols, R, hipMemcpyHostToDevice, ctx->stream);
+      if (e == hipSuccess) {
+        hipLaunchKernelGGL(transpose_kernel<true>, grid, dim3(256), 0, ctx->stream,
+                           (const double*)stage, ctx->A + i0, R, cols, cols, ctx->ld);
+        e = hipGetLastError();
+      }
+    } else {
+      hipLaunchKernelGGL(transpose_kernel<false>, grid, dim3(256), 0, ctx->stream,
+                         (const double*)(ctx->A + i0), stage, R, cols, cols, ctx->ld);
+      e = hipGetLastError();
+      if (e == hipSuccess)
+        e = hipMemcpy2DAsync(host + i0 * ld, sizeof(double) * ld, stage, sizeof(double) * cols,
+                             sizeof(double) * cols, R, hipMemcpyDeviceToHost, ctx->stream);
+    }
+    // (the staging buffer is reused by the next chunk: wait for this one)
+    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+    if (e != hipSuccess) {
+      ctx->err = std::string("row transfer: ") + hipGetErrorString(e);
+      rc = SPX_E_HIP;
+    }
+  }
+  (void)hipFree(stage);
+  return rc;
+}
+
 int spx_load_rows(spx_ctx* ctx, const double* A, int64_t m_local, int64_t cols, int64_t ld,
                   int layout, const double* obj, const int64_t* basis, int64_t m_global,
                   int64_t row0) {
@@ -1789,22 +1831,18 @@ int spx_load_rows(spx_ctx* ctx, const double* A, int64_t m_local, int64_t cols, 
   int rc = alloc_common(ctx, m_local, cols, m_global, row0);
   if (rc) return rc;
   if (m_local > 0) {
+    // the column padding rows (ld > m_local) hold zeros, whatever the buffer held
+    if (ctx->ld > m_local) HIPC(hipMemsetAsync(ctx->A, 0, ctx->A_bytes, ctx->stream));
     if (layout == SPX_COL_MAJOR) {
       HIPC(hipMemcpy2DAsync(ctx->A, sizeof(double) * ctx->ld, A, sizeof(double) * ld,
                             sizeof(double) * m_local, cols, hipMemcpyHostToDevice,
                             ctx->stream));
     } else {
-      // blocked host transpose into a column-major staging buffer
-      std::vector<double> stage((size_t)ctx->ld * cols, 0.0);
-      const int64_t B = 64;
-      for (int64_t i0 = 0; i0 < m_local; i0 += B)
-        for (int64_t j0 = 0; j0 < cols; j0 += B)
-          for (int64_t i = i0; i < std::min(i0 + B, m_local); ++i)
-            for (int64_t j = j0; j < std::min(j0 + B, cols); ++j)
-              stage[(size_t)j * ctx->ld + i] = A[i * ld + j];
-      HIPC(hipMemcpyAsync(ctx->A, stage.data(), sizeof(double) * stage.size(),
-                          hipMemcpyHostToDevice, ctx->stream));
-      HIPC(hipStreamSynchronize(ctx->stream));
+      // row-major host rows: copied in chunks into a device staging buffer,
+      // transposed there into the column-major tableau (the host transpose
+      // this replaces ran at ~2 GB/s; tools/pcie_rate.py)
+      rc = transfer_rows(ctx, const_cast<double*>(A), m_local, cols, ld, true);
+      if (rc) return rc;
     }
   }
   HIPC(hipMemcpyAsync(ctx->obj, obj, sizeof(double) * cols, hipMemcpyHostToDevice, ctx->stream));
@@ -1844,21 +1882,25 @@ int spx_get_tableau(spx_ctx* ctx, double* out, int64_t ld, int layout) {
   CHECK_ARG(layout == SPX_ROW_MAJOR || layout == SPX_COL_MAJOR, "bad layout");
   const int64_t rows = ctx->m_local + 1, N = ctx->N;
   CHECK_ARG(layout == SPX_ROW_MAJOR ? ld >= N : ld >= rows, "bad ld");
-  std::vector<double> stage((size_t)ctx->ld * N), o((size_t)N);
-  HIPC(hipMemcpyAsync(stage.data(), ctx->A, sizeof(double) * stage.size(),
-                      hipMemcpyDeviceToHost, ctx->stream));
-  HIPC(hipMemcpyAsync(o.data(), ctx->obj, sizeof(double) * N, hipMemcpyDeviceToHost,
-                      ctx->stream));
-  HIPC(hipStreamSynchronize(ctx->stream));
-  for (int64_t j = 0; j < N; ++j) {
-    for (int64_t i = 0; i < ctx->m_local; ++i) {
-      const double v = stage[(size_t)j * ctx->ld + i];
-      if (layout == SPX_ROW_MAJOR) out[i * ld + j] = v;
-      else out[j * ld + i] = v;
+  const int64_t ml = ctx->m_local;
+  if (layout == SPX_ROW_MAJOR) {
+    // rows through a device transpose and one 2-D copy per chunk (the host
+    // transpose this replaces ran at ~2 GB/s; tools/pcie_rate.py)
+    if (ml > 0) {
+      const int rc = transfer_rows(ctx, out, ml, N, ld, false);
+      if (rc) return rc;
     }
-    if (layout == SPX_ROW_MAJOR) out[ctx->m_local * ld + j] = o[j];
-    else out[j * ld + ctx->m_local] = o[j];
+    HIPC(hipMemcpyAsync(out + ml * ld, ctx->obj, sizeof(double) * N, hipMemcpyDeviceToHost,
+                        ctx->stream));
+  } else {
+    if (ml > 0)
+      HIPC(hipMemcpy2DAsync(out, sizeof(double) * ld, ctx->A, sizeof(double) * ctx->ld,
+                            sizeof(double) * ml, N, hipMemcpyDeviceToHost, ctx->stream));
+    // the objective row: one element per column, ld apart
+    HIPC(hipMemcpy2DAsync(out + ml, sizeof(double) * ld, ctx->obj, sizeof(double),
+                          sizeof(double), N, hipMemcpyDeviceToHost, ctx->stream));
   }
+  HIPC(hipStreamSynchronize(ctx->stream));
   return SPX_OK;
 }
 

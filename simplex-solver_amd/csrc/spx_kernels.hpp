@@ -41,6 +41,42 @@ namespace spx {
 constexpr int BLK = 256;  // threads per workgroup (4 wave64)
 constexpr int NWAVE = BLK / 64;
 
+// Row-major <-> column-major transposes of the boundary (spx_load_rows /
+// spx_get_tableau with SPX_ROW_MAJOR): 32 x 32 tiles through LDS (a padded
+// row, so the column reads do not share a bank), 32 x 8 threads, so both the
+// row-major and the column-major side move 256-B runs.  rm: R x C row-major,
+// pitch prm doubles; cm: column-major, pitch pcm doubles (element (i, j) at
+// cm[j * pcm + i]).  TO_CM: rm -> cm, else cm -> rm.
+template <bool TO_CM>
+__global__ __launch_bounds__(256) void transpose_kernel(const double* __restrict__ src,
+                                                        double* __restrict__ dst, int64_t R,
+                                                        int64_t C, int64_t prm, int64_t pcm) {
+  __shared__ double tile[32][33];
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+  const int64_t i0 = (int64_t)blockIdx.y * 32, j0 = (int64_t)blockIdx.x * 32;
+  if constexpr (TO_CM) {
+    for (int y = ty; y < 32; y += 8) {  // rows i0 + y, columns j0 + tx
+      const int64_t i = i0 + y, j = j0 + tx;
+      if (i < R && j < C) tile[y][tx] = src[i * prm + j];
+    }
+    __syncthreads();
+    for (int y = ty; y < 32; y += 8) {  // columns j0 + y, rows i0 + tx
+      const int64_t i = i0 + tx, j = j0 + y;
+      if (i < R && j < C) dst[j * pcm + i] = tile[tx][y];
+    }
+  } else {
+    for (int y = ty; y < 32; y += 8) {  // columns j0 + y, rows i0 + tx
+      const int64_t i = i0 + tx, j = j0 + y;
+      if (i < R && j < C) tile[tx][y] = src[j * pcm + i];
+    }
+    __syncthreads();
+    for (int y = ty; y < 32; y += 8) {  // rows i0 + y, columns j0 + tx
+      const int64_t i = i0 + y, j = j0 + tx;
+      if (i < R && j < C) dst[i * prm + j] = tile[y][tx];
+    }
+  }
+}
+
 // device-side solve status (mapped to SPX_* codes on the host)
 constexpr int32_t ST_RUNNING = 0;
 constexpr int32_t ST_OPTIMAL = 1;

@@ -29,11 +29,14 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--windows", type=int, default=20)
     ap.add_argument("--full", action="store_true", help="also solve to optimality")
+    ap.add_argument("--order", default="F", choices=["F", "C"],
+                    help="host layout of the tableau: F column-major, C row-major (numpy's default)")
     a = ap.parse_args()
     K, m, n, seed = 24, 8192, 8192, 20251205
-    Tf, obj, basis = synth.tableau_rows("dense", m, n, seed, order="F")
+    Tf, obj, basis = synth.tableau_rows("dense", m, n, seed, order=a.order)
     nbytes = Tf.nbytes + obj.nbytes
     out = {"tool": "pcie_rate", "config": "config 3: 8192x16385 fp64", "window": K,
+           "host_order": a.order,
            "tableau_bytes": int(nbytes)}
     with DeviceTableau(0) as e:
         e.set_window(K)
