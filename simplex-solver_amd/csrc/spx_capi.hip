@@ -1781,8 +1781,10 @@ int spx_destroy(spx_ctx* ctx) {
 // into the staging buffer, then a 2-D copy into the host rows (pitch ld).
 int transfer_rows(spx_ctx* ctx, double* host, int64_t nrows, int64_t cols, int64_t ld,
                   bool to_device) {
-  const int64_t chunk = std::max<int64_t>(32, std::min<int64_t>(
-                                                  nrows, ((8 << 20) / cols + 31) / 32 * 32));
+  // (rows per chunk: ~64 MB of staging, at most 65535 tiles of 32 rows -- the
+  // grid's y limit)
+  const int64_t chunk = std::min<int64_t>(
+      65535 * 32, std::max<int64_t>(32, std::min<int64_t>(nrows, ((8 << 20) / cols + 31) / 32 * 32)));
   double* stage = nullptr;
   HIPC(hipMalloc(&stage, sizeof(double) * chunk * cols));
   int rc = SPX_OK;
