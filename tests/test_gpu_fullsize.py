@@ -73,11 +73,13 @@ def _full_solve(name, window=24, chain=0):
     return fx
 
 
-@pytest.mark.parametrize("window,chain", [(24, 0), (28, 0)], ids=["k24", "k28"])
+@pytest.mark.parametrize("window,chain", [(24, 0), (28, 0), (32, 0), (16, 0), (24, 1), (0, 0)],
+                         ids=["k24", "k28", "k32", "k16", "k24_launch_per_phase", "single_pivot"])
 def test_config3_dantzig_full_solve_pinned(window, chain):
     """Config 3 (8192 x 8192 dense LP, tableau 8193 x 16385): the whole
-    Dantzig solve at K = 24 and 28 (the LEAN slot chains) vs the oracle's,
-    index for index."""
+    Dantzig solve vs the oracle's, index for index, at K = 16 / 24 / 28 / 32
+    (the LEAN slot chains), with the launch-per-phase chain (mode 1), and one
+    pivot per tableau pass (window 0)."""
     _full_solve("config3", window=window, chain=chain)
 
 
