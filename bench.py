@@ -19,7 +19,9 @@ and `cpu_baseline` (rank 0 at N=1 only): the C/OpenMP restatement of the
 oracle (oracle/spx_oracle.c) on a bounded sample of the same workload with
 this job's CPU share (OMP_NUM_THREADS threads), beside the same C code on 1
 thread and the numpy oracle on 1 thread; every sample's pivots must equal the
-GPU's.
+GPU's.  `cpu_baseline.highs`: the reference's own engine (scipy linprog
+'highs-ds', HiGHS) on config 2 beside the GPU's solve of the same LP; the
+host load average is recorded beside every CPU figure.
 
 At N > 1 the row-sharded persistent chain first passes a self-test on a small
 LP (both leaving-row transports, pull and owner-push, byte-identical to the
@@ -144,9 +146,12 @@ def cpu_baseline(m, n, seed, rule, budget_s, gpu_hist):
 
     threads = C.threads()  # OMP_NUM_THREADS
     Tc, bc, hist = T.copy(), basis0.copy(), []
+    la0 = _loadavg()
     k, el = c_run(threads, budget_s * 0.6, Tc, bc, hist)
+    la1 = _loadavg()
     # 1 thread, continuing the same sequence
     k1, el1 = c_run(1, budget_s * 0.2, Tc, bc, hist)
+    la2 = _loadavg()
     # the thread-scaling curve between them (short samples, same sequence)
     scaling = {"1": k1 / el1 if el1 > 0 else None, str(threads): k / el}
     for tt in (2, 4, 8):
@@ -167,19 +172,75 @@ def cpu_baseline(m, n, seed, rule, budget_s, gpu_hist):
         k2 += 1
     el2 = time.perf_counter() - t0
     ok2 = matches(hist2)
+    la3 = _loadavg()
     host = _host_cpus()
     return {"value": k / el, "unit": "pivots/s", "cores": threads, "kind": "port",
             "sample": f"C/OpenMP oracle (oracle/spx_oracle.c), first {k} {rule} pivots of the "
                       f"same {m}x{n} tableau from the slack basis, {el:.1f} s, {threads} threads "
                       f"(this job's CPU share)",
+            # host load (1/5/15-min os.getloadavg) before and after each sample:
+            # the box's other jobs share its cores, and the figures move with them
+            "loadavg": {"before": la0, "after": la1},
             "pivot_sequence_matches_gpu": bool(ok and ok2),
             "c_1thread": {"value": k1 / el1 if el1 > 0 else None, "pivots": k1,
-                          "seconds": el1},
+                          "seconds": el1, "loadavg": {"before": la1, "after": la2}},
             "numpy_1thread": {"value": k2 / el2, "pivots": k2, "seconds": el2,
-                              "matches_gpu": bool(ok2)},
+                              "matches_gpu": bool(ok2), "loadavg": {"before": la2, "after": la3}},
             "all_cores": _all_cores_projection(k / el, threads, host, alg_bytes_per_pivot(m, n),
                                                scaling),
             "host": host}
+
+
+def _loadavg():
+    try:
+        return [round(x, 2) for x in os.getloadavg()]
+    except OSError:
+        return None
+
+
+# BASELINE.json config 2 (seed 20251205 + its index, as tools/bench_configs.py)
+CONFIG2 = (1024, 2048, 20251207)
+
+
+def highs_beside(window):
+    """The reference's real answer engine beside the GPU, on config 2 (rank 0,
+    N = 1, after the timed region): scipy linprog(method='highs-ds') called as
+    /root/reference/app/controllers/solver_controller.py:76-85 calls it (max
+    -> negated c, A_ub / b_ub, bounds (0, None), presolve on) with the 10 s
+    time_limit lifted, against this build's GPU engine solving the same LP to
+    optimality through the C-ABI (K-pivot windows, the tableau loaded before
+    the clock starts, as `value`).  Wall times, pivots / iterations, the two
+    objectives and the host load."""
+    from scipy.optimize import linprog
+    from simplex_amd import synth
+    from simplex_amd.engine import DeviceTableau
+    m, n, seed = CONFIG2
+    T, basis = synth.full_tableau("dense", m, n, seed)
+    with DeviceTableau(0) as e:
+        e.set_window(window)
+        e.load(T, basis)
+        e.solve(max_iters=5)  # warm: graph build, first launches
+        e.load(T, basis)
+        t0 = time.perf_counter()
+        res = e.solve()
+        gpu_s = time.perf_counter() - t0
+    A, b, c = synth.lp_data("dense", m, n, seed)
+    la0 = _loadavg()
+    t0 = time.perf_counter()
+    h = linprog(-c, A_ub=A, b_ub=b, bounds=[(0, None)] * n, method="highs-ds",
+                options={"presolve": True})
+    highs_s = time.perf_counter() - t0
+    z = -h.fun
+    return {"what": "scipy linprog(method='highs-ds') (HiGHS dual simplex, the reference's "
+                    "answer path, solver_controller.py:76-85; time_limit lifted) on config 2 "
+                    "vs this build's GPU solve of the same LP to optimality",
+            "lp": f"config 2: {m}x{n} dense random-feasible LP (seed {seed})",
+            "highs_seconds": highs_s, "highs_nit": int(h.nit), "highs_objective": z,
+            "highs_status": int(h.status), "gpu_seconds": gpu_s, "gpu_pivots": int(res.iters),
+            "gpu_objective": res.objective, "gpu_window": window,
+            "objective_rel_diff": abs(res.objective - z) / abs(z),
+            "gpu_speedup_wall": highs_s / gpu_s if gpu_s > 0 else None,
+            "cores": 1, "loadavg": {"before": la0, "after": _loadavg()}}
 
 
 # The pivot chain's latency floor per pivot (MI355X_MICROARCH.md price list,
@@ -534,6 +595,10 @@ def main():
     cpu = None
     if hist is not None and world == 1 and args.cpu_seconds > 0:
         cpu = cpu_baseline(m, n, args.seed, args.rule, args.cpu_seconds, hist.tolist())
+        try:
+            cpu["highs"] = highs_beside(K if K else 24)
+        except Exception as ex:  # scipy missing or failed: say so, keep the line
+            cpu["highs"] = {"error": f"{type(ex).__name__}: {ex}"}
     if rank == 0:
         value = n_timed / elapsed
         fvar = eng.elim_variant()

@@ -155,6 +155,11 @@ int spx_get_peer_push(spx_ctx* ctx, int* on);
  * pointers as mapped here (out[3+2q], out[4+2q]; 0 before an import).
  * n >= 3 + 2 * nranks. */
 int spx_peer_debug(spx_ctx* ctx, uint64_t* out, int n);
+/* Diagnostic: out[0] buffers this context ever exported, out[1] buffers in its
+ * pool, out[2] ever-exported buffers it still holds (pooled or loaded); an
+ * exported buffer is never freed before spx_destroy, so out[0] == out[2].
+ * n >= 3. */
+int spx_peer_pool_debug(spx_ctx* ctx, uint64_t* out, int n);
 
 /* ---- data in / out ------------------------------------------------------- */
 /* Load a full tableau of `rows` = m+1 rows (objective row LAST) and `cols` = N
@@ -254,6 +259,14 @@ int spx_get_flush_variant(const spx_ctx* ctx, int64_t out[4]);
  * Results are bit-identical.  Row-sharded contexts run the
  * same windows with one all-gather per pivot. */
 int spx_set_window(spx_ctx* ctx, int K);
+/* The row_fix fold: on = 1, a window's fast-path
+ * leaving rows are rewritten by the NEXT window's persistent chain launch
+ * (each thread its own column, before the start handshake) and after a
+ * call's last window by one row_fix launch; on = 0 (default), a row_fix
+ * launch after every window.  Single-GPU persistent chains with 256-thread
+ * blocks only; bit-identical either way.  Measured no faster on config 3
+ * (the fix's ~13 us moves onto the chain's critical path), hence off. */
+int spx_set_row_fix_fold(spx_ctx* ctx, int on);
 /* Pivot-choice timing (diagnostic): when on, every window records HIP events
  * around its chain (the persistent kernel, or the lazy kernels of its slots);
  * spx_chain_timing returns their sum and count since the last reset.  The

@@ -140,7 +140,17 @@ struct spx_ctx {
 
   // windowed (delayed) elimination: 0 = off (fused per-pivot elimination)
   int win_k = 0;
-  Window win{};
+  // two sets of per-window buffers, alternating by window (wpar: the set of
+  // the next window), so window w's buffers survive window w+1's chain, which
+  // resolves w's leaving rows (the row_fix fold).  last_fold:
+  // the last enqueued window was a fold window (its set may owe its fix: a
+  // gated row_fix settles it before a window that is not one, and at the end
+  // of every call).  fold: use fold windows (spx_set_row_fix_fold; the
+  // persistent single-GPU chain only).
+  Window wins[2]{};
+  int wpar = 0;
+  bool last_fold = false;
+  int fold = 0;  // (off by default: measured no faster)
   // persistent pivot chain of a window (spx_chain.hpp): record buffers and mode
   unsigned long long* gr_enter = nullptr;  // ENTER_REC x CHAIN_MAX_BLOCKS granules
   unsigned long long* gr_ratio = nullptr;  // RATIO_REC x CHAIN_MAX_BLOCKS granules
@@ -175,12 +185,20 @@ struct spx_ctx {
   // role holds at most POOL_MAX buffers: a load needing another fails with
   // SPX_E_STATE instead of growing.  spx_destroy first waits (bounded) for
   // every peer's release mark (close_peers), then frees everything.
-  bool exported = false;
+  // Every buffer spx_peer_export ever exported stays in `ever_exported`, so a
+  // buffer taken from the pool and not exported again (a load whose import
+  // was skipped or failed, or an alloc_common that failed after pool_take)
+  // still goes back to the pool, never to hipFree.
+  std::set<void*> ever_exported;
+  bool imported_load = false;   // an spx_peer_import succeeded since the current load
   uint32_t peer_gen = 0;        // successful IPC imports of this context (the same on every rank)
   struct Pooled {
     void* p;
     size_t bytes;
     int role;                   // POOL_TABLEAU / POOL_RECORDS (its allocation flags follow)
+    uint32_t gen;               // records: the import generation whose release marks it
+                                // receives (peers write them when they close that mapping);
+                                // 0 if it was never imported
   };
   std::vector<Pooled> pool;
   int peer_push = 0;            // leaving-row transport requested for the next import (spx_set_peer_push)
@@ -201,7 +219,14 @@ struct spx_ctx {
   // captured launch sequences by chunk (pivots): a few sizes per context
   // (the bench's warmup and timed runs, spx_solve), so none is rebuilt inside
   // a timed region
-  std::map<int, hipGraphExec_t> graphs;
+  // (key: chunk, the window set parity and last_fold the capture began with;
+  // value: the graph and the host state its replay leaves: parity, last_fold)
+  struct GraphEntry {
+    hipGraphExec_t exec;
+    int par_after;
+    bool fold_after;
+  };
+  std::map<int64_t, GraphEntry> graphs;
   hipGraphExec_t gexec = nullptr;  // the one build_graph returned last
   // windows per replayed graph (SPX_GRAPH_WINDOWS): consecutive windows in one
   // graph pay one graph-launch gap (8.4 us at config 3) instead of one each
@@ -253,12 +278,12 @@ void dfree(T*& p) {
 }
 
 void drop_graphs(spx_ctx* ctx) {
-  for (auto& kv : ctx->graphs) (void)hipGraphExecDestroy(kv.second);
+  for (auto& kv : ctx->graphs) (void)hipGraphExecDestroy(kv.second.exec);
   ctx->graphs.clear();
   ctx->gexec = nullptr;
 }
 
-// IPC release marks (spx_ctx::exported): granule {CLOSE_TAG, generation} at
+// IPC release marks (spx_ctx::ever_exported): granule {CLOSE_TAG, generation} at
 // slot `rank` of each peer's release plane, written through this rank's
 // mapping of that peer's record buffer before the mapping is closed.
 constexpr unsigned CLOSE_TAG = 0xC105ED00u;
@@ -284,41 +309,45 @@ void close_peers(spx_ctx* ctx) {
   ctx->peer_B = 0;
 }
 
-// Every peer's release mark for this context's current import generation, in
-// its own record buffer (bounded wait).  True when all arrived.
-bool wait_peer_release(spx_ctx* ctx, double seconds) {
-  if (ctx->nranks <= 1 || !ctx->gr_ratio) return true;
+// Every peer's release mark for import generation `gen` in the record buffer
+// `rec` (one this context exported; peers write the marks through their
+// mapping of it when they close that mapping), until `deadline`.  True when
+// all arrived.
+bool wait_peer_release(spx_ctx* ctx, const unsigned long long* rec, uint32_t gen,
+                       std::chrono::steady_clock::time_point deadline) {
+  if (ctx->nranks <= 1 || !rec || gen == 0) return true;
   std::vector<unsigned long long> h((size_t)ctx->nranks);
-  const auto t0 = std::chrono::steady_clock::now();
   for (;;) {
-    if (hipMemcpy(h.data(), ctx->gr_ratio + (size_t)CLOSE_PLANE_SHARD * CHAIN_SH_SLOTS,
+    if (hipMemcpy(h.data(), rec + (size_t)CLOSE_PLANE_SHARD * CHAIN_SH_SLOTS,
                   sizeof(unsigned long long) * h.size(), hipMemcpyDeviceToHost) != hipSuccess)
       return false;
     bool all = true;
     for (int q = 0; q < ctx->nranks; ++q)
-      if (q != ctx->rank)
-        all &= (unsigned)(h[q] >> 32) == CLOSE_TAG && (uint32_t)h[q] == ctx->peer_gen;
+      if (q != ctx->rank) all &= (unsigned)(h[q] >> 32) == CLOSE_TAG && (uint32_t)h[q] == gen;
     if (all) return true;
-    if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > seconds)
-      return false;
+    if (std::chrono::steady_clock::now() > deadline) return false;
     std::this_thread::sleep_for(std::chrono::microseconds(200));
   }
 }
 
-// Frees the loaded tableau's buffers; an exported tableau and record buffer
-// go to the context's pool instead (spx_ctx::pool).
+// Frees the loaded tableau's buffers; a tableau or record buffer that was
+// ever exported goes to the context's pool instead (spx_ctx::pool), whether or
+// not the current load exported it again.
 constexpr int POOL_TABLEAU = 0, POOL_RECORDS = 1, POOL_MAX = 4;
 int free_buffers(spx_ctx* ctx) {
   drop_graphs(ctx);
   close_peers(ctx);
-  const char* keep = std::getenv("SPX_IPC_KEEP");  // diagnostic: 0 = free them (unsafe)
-  if (ctx->exported && !(keep && keep[0] == '0')) {
-    if (ctx->A) ctx->pool.push_back({ctx->A, ctx->A_bytes, POOL_TABLEAU});
-    if (ctx->gr_ratio) ctx->pool.push_back({ctx->gr_ratio, ctx->gr_bytes, POOL_RECORDS});
+  if (ctx->A && ctx->ever_exported.count(ctx->A)) {
+    ctx->pool.push_back({ctx->A, ctx->A_bytes, POOL_TABLEAU, 0u});
     ctx->A = nullptr;
+  }
+  if (ctx->gr_ratio && ctx->ever_exported.count(ctx->gr_ratio)) {
+    // (peers that imported this load write their release marks into it)
+    ctx->pool.push_back({ctx->gr_ratio, ctx->gr_bytes, POOL_RECORDS,
+                         ctx->imported_load ? ctx->peer_gen : 0u});
     ctx->gr_ratio = nullptr;
   }
-  ctx->exported = false;
+  ctx->imported_load = false;
   dfree(ctx->A);
   dfree(ctx->obj);
   dfree(ctx->F);
@@ -330,15 +359,25 @@ int free_buffers(spx_ctx* ctx) {
   dfree(ctx->ratio_part);
   dfree(ctx->sendbuf);
   dfree(ctx->recvbuf);
-  dfree(ctx->win.F);
-  dfree(ctx->win.P);
-  dfree(ctx->win.r);
-  dfree(ctx->win.c);
-  dfree(ctx->win.made);
-  dfree(ctx->win.tag);
-  dfree(ctx->win.epoch);
-  dfree(ctx->win.nlist);
-  dfree(ctx->win.rec);
+  for (Window& w : ctx->wins) {
+    dfree(w.F);
+    dfree(w.P);
+    dfree(w.r);
+    dfree(w.c);
+    dfree(w.made);
+    dfree(w.nlist);
+    dfree(w.rec);
+    dfree(w.frt);
+    dfree(w.Pf);
+  }
+  dfree(ctx->wins[0].tag);
+  dfree(ctx->wins[0].epoch);
+  dfree(ctx->wins[0].fix);
+  ctx->wins[1].tag = nullptr;
+  ctx->wins[1].epoch = nullptr;
+  ctx->wins[1].fix = nullptr;
+  ctx->wpar = 0;
+  ctx->last_fold = false;
   dfree(ctx->gr_enter);
   dfree(ctx->gr_ratio);
   ctx->loaded = false;
@@ -905,11 +944,52 @@ int next_event_pair(spx_ctx* ctx, std::vector<std::pair<hipEvent_t, hipEvent_t>>
   return SPX_OK;
 }
 
+// The gated row_fix of window set `sid` (the row_fix fold):
+// rewrites its leaving rows only if that set's fold chain left them owed.
+template <int KMAX>
+void launch_gated_fix_t(spx_ctx* ctx, int sid) {
+  hipLaunchKernelGGL((row_fix_kernel<KMAX, BLK, true>), dim3(ctx->nbn), dim3(BLK), 0,
+                     ctx->stream, ctx->A, ctx->ld, ctx->m_local, ctx->row0, ctx->N,
+                     ctx->wins[sid], KMAX);
+}
+void launch_gated_fix(spx_ctx* ctx, int sid) {
+  switch (ctx->win_k) {
+    case 2: return launch_gated_fix_t<2>(ctx, sid);
+    case 4: return launch_gated_fix_t<4>(ctx, sid);
+    case 8: return launch_gated_fix_t<8>(ctx, sid);
+    case 12: return launch_gated_fix_t<12>(ctx, sid);
+    case 16: return launch_gated_fix_t<16>(ctx, sid);
+    case 24: return launch_gated_fix_t<24>(ctx, sid);
+    case 28: return launch_gated_fix_t<28>(ctx, sid);
+    default: return launch_gated_fix_t<32>(ctx, sid);
+  }
+}
+
+// The end of a call's enqueued windows (and before anything reads or changes
+// the tableau outside the windows): the last window, if a fold window, owes
+// its leaving rows' fix -- settle it on the stream.
+int settle_fold(spx_ctx* ctx) {
+  if (!ctx->last_fold) return SPX_OK;
+  launch_gated_fix(ctx, ctx->wpar ^ 1);
+  ctx->last_fold = false;
+  HIPC(hipGetLastError());
+  return SPX_OK;
+}
+
 template <int KMAX>
 int enqueue_window_t(spx_ctx* ctx, int npiv, bool time_flush) {
   const int nbw = lazy_ratio_grid(ctx);
   int cb = BLK;
   const int B = chain_blocks(ctx, &cb);
+  // this window's buffer set and the previous window's (the host's parity)
+  const int S = ctx->wpar, P = S ^ 1;
+  const Window& win = ctx->wins[S];
+  // the row_fix fold: the persistent single-GPU chain with
+  // 256-thread blocks resolves the previous window's leaving rows itself
+  const bool fold = ctx->fold && B > 0 && !ctx->sharded && cb == 256;
+  // a window that is not a fold window reads a tableau whose leaving rows are
+  // all fixed: settle what the last fold window owes first
+  if (!fold && ctx->last_fold) launch_gated_fix(ctx, P);
   std::pair<hipEvent_t, hipEvent_t>* ec = nullptr;
   if (ctx->time_chain) {
     int rc = next_event_pair(ctx, ctx->evc, ctx->evc_used, &ec);
@@ -921,12 +1001,13 @@ int enqueue_window_t(spx_ctx* ctx, int npiv, bool time_flush) {
     const int rpb = (int)std::max<int64_t>(1, (ctx->m_local + B - 1) / B);
     auto kern = ctx->sharded ? (cb == 512 ? chain_shard_kernel<KMAX, 512>
                                           : chain_shard_kernel<KMAX, 256>)
-                             : (cb == 512 ? chain_kernel<KMAX, 512> : chain_kernel<KMAX, 256>);
+                : fold ? chain_kernel<KMAX, 256, true>
+                       : (cb == 512 ? chain_kernel<KMAX, 512> : chain_kernel<KMAX, 256>);
     hipLaunchKernelGGL(kern, dim3(B), dim3(cb), 0, ctx->stream, ctx->enter_part, ctx->st,
                        (const Params*)ctx->prm, std::max(NWAVE * ctx->nbn, B),
-                       (const double*)ctx->A, ctx->ld, ctx->m_local, ctx->N, ctx->obj, ctx->win,
+                       (const double*)ctx->A, ctx->ld, ctx->m_local, ctx->N, ctx->obj, win,
                        npiv, ctx->basis, ctx->hist, ctx->gr_enter, ctx->gr_ratio, cpb, rpb,
-                       (const ChainPeers*)ctx->d_peers);
+                       (const ChainPeers*)ctx->d_peers, ctx->wins[P], 0, ctx->A);
   } else if (ctx->sharded && !ctx->comm && !ctx->loop) {
     ctx->err = "a peer-only shard needs the persistent chain (windowed, spx_peer_import done, "
                "chain mode != 1, and its grid fits)";
@@ -936,13 +1017,13 @@ int enqueue_window_t(spx_ctx* ctx, int npiv, bool time_flush) {
     hipLaunchKernelGGL(lazy_ratio_kernel<KMAX>, dim3(nbw), dim3(BLK), 0, ctx->stream,
                        (const Key*)ctx->enter_part, ctx->st, (const Params*)ctx->prm,
                        NWAVE * ctx->nbn, q, (const double*)ctx->A, ctx->ld, ctx->m_local,
-                       ctx->row0, ctx->N, (const double*)ctx->obj, ctx->win, ctx->ratio_part,
+                       ctx->row0, ctx->N, (const double*)ctx->obj, win, ctx->ratio_part,
                        (const int64_t*)ctx->basis);
     if (!ctx->sharded) {
       hipLaunchKernelGGL(lazy_norm_kernel<KMAX>, dim3(ctx->nbn), dim3(BLK), 0, ctx->stream,
                          (const Key*)ctx->ratio_part, ctx->st, (const Params*)ctx->prm,
                          NWAVE * nbw, q, (const double*)ctx->A, ctx->ld, ctx->m_local,
-                         ctx->row0, ctx->N, ctx->obj, ctx->win, npiv - 1, ctx->enter_part,
+                         ctx->row0, ctx->N, ctx->obj, win, npiv - 1, ctx->enter_part,
                          ctx->basis, ctx->hist, nullptr, (int64_t)0, 0);
     } else {
       // row shard: local candidate row (current values) -> ONE all-gather of
@@ -950,14 +1031,14 @@ int enqueue_window_t(spx_ctx* ctx, int npiv, bool time_flush) {
       hipLaunchKernelGGL(lazy_prep_kernel<KMAX>, dim3(ctx->nbn), dim3(BLK), 0, ctx->stream,
                          (const Key*)ctx->ratio_part, (const State*)ctx->st,
                          (const Params*)ctx->prm, NWAVE * nbw, q, (const double*)ctx->A,
-                         ctx->ld, ctx->m_local, ctx->row0, ctx->N, ctx->win, ctx->sendbuf,
+                         ctx->ld, ctx->m_local, ctx->row0, ctx->N, win, ctx->sendbuf,
                          ctx->rank, (const int32_t*)ctx->d_stop);
       const int rc = comm_allgather(ctx);
       if (rc) return rc;
       hipLaunchKernelGGL((lazy_norm_kernel<KMAX, true>), dim3(ctx->nbn), dim3(BLK), 0,
                          ctx->stream, (const Key*)ctx->ratio_part, ctx->st,
                          (const Params*)ctx->prm, NWAVE * nbw, q, (const double*)ctx->A,
-                         ctx->ld, ctx->m_local, ctx->row0, ctx->N, ctx->obj, ctx->win,
+                         ctx->ld, ctx->m_local, ctx->row0, ctx->N, ctx->obj, win,
                          npiv - 1, ctx->enter_part, ctx->basis, ctx->hist,
                          (const char*)ctx->recvbuf, ctx->gstride, ctx->nranks);
     }
@@ -978,7 +1059,7 @@ int enqueue_window_t(spx_ctx* ctx, int npiv, bool time_flush) {
     ctx->last_flush_G = G;
     ctx->last_flush_rch = rch;
     hipLaunchKernelGGL(kern, dim3(rch * G), dim3(threads), 0, ctx->stream, ctx->A, ctx->ld,
-                       ctx->m_local, ctx->row0, ctx->N, ctx->win, npiv, rch, G, ctx->prm,
+                       ctx->m_local, ctx->row0, ctx->N, win, npiv, rch, G, ctx->prm,
                        ctx->st, ctx->flush_map | ctx->flush_tail << 8);
   };
   const bool nts = (ctx->elim_nt & 2) != 0;
@@ -995,9 +1076,13 @@ int enqueue_window_t(spx_ctx* ctx, int npiv, bool time_flush) {
   }
   // the fast-path columns' leaving rows (every window: partial ones included);
   // a tail inside the flush measured 226 vs 182 us
-  // (profiles/r03/ab_flush_tail_vs_rowfix.jsonl)
-  hipLaunchKernelGGL(row_fix_kernel<KMAX>, dim3(ctx->nbn), dim3(BLK), 0, ctx->stream, ctx->A,
-                     ctx->ld, ctx->m_local, ctx->row0, ctx->N, ctx->win, npiv);
+  // (profiles/r03/ab_flush_tail_vs_rowfix.jsonl).  A fold window leaves them
+  // to the next fold chain (or the gated row_fix of settle_fold).
+  if (!fold)
+    hipLaunchKernelGGL(row_fix_kernel<KMAX>, dim3(ctx->nbn), dim3(BLK), 0, ctx->stream, ctx->A,
+                       ctx->ld, ctx->m_local, ctx->row0, ctx->N, win, npiv);
+  ctx->last_fold = fold;
+  ctx->wpar = P;
   HIPC(hipGetLastError());
   return SPX_OK;
 }
@@ -1153,17 +1238,32 @@ int begin_call(spx_ctx* ctx, const spx_opts* o, AdmCall* adm_call, int64_t fc = 
   return SPX_OK;
 }
 
-int build_graph(spx_ctx* ctx, int chunk) {
-  const auto it = ctx->graphs.find(chunk);
+// The captured graph of `chunk` pivots for the current host window state (the
+// next window's buffer set, and whether the last window was a fold window):
+// its launches bake in the sets they use, so each state has its own graph.
+int64_t graph_key(const spx_ctx* ctx, int chunk, int par, bool fold) {
+  return ((int64_t)chunk << 2) | (par << 1) | (fold ? 1 : 0);
+}
+int build_graph_for(spx_ctx* ctx, int chunk, int par, bool fold) {
+  const auto it = ctx->graphs.find(graph_key(ctx, chunk, par, fold));
   if (it != ctx->graphs.end()) {
-    ctx->gexec = it->second;
+    ctx->gexec = it->second.exec;
     return SPX_OK;
   }
   ctx->gexec = nullptr;
+  // capture from that state; the host state returns to where it was (the
+  // graph's launches advance it, launch_graph)
+  const int par0 = ctx->wpar;
+  const bool fold0 = ctx->last_fold;
+  ctx->wpar = par;
+  ctx->last_fold = fold;
   hipGraph_t g = nullptr;
   HIPC(hipStreamBeginCapture(ctx->stream, hipStreamCaptureModeThreadLocal));
   int rc = enqueue_pivots(ctx, chunk, 0);
   hipError_t e = hipStreamEndCapture(ctx->stream, &g);
+  const spx_ctx::GraphEntry ge{nullptr, ctx->wpar, ctx->last_fold};
+  ctx->wpar = par0;
+  ctx->last_fold = fold0;
   if (rc) {
     if (g) (void)hipGraphDestroy(g);
     return rc;
@@ -1179,7 +1279,31 @@ int build_graph(spx_ctx* ctx, int chunk) {
     ctx->err = std::string("hipGraphInstantiate: ") + hipGetErrorString(e);
     return SPX_E_HIP;
   }
-  ctx->graphs[chunk] = ctx->gexec;
+  spx_ctx::GraphEntry en = ge;
+  en.exec = ctx->gexec;
+  ctx->graphs[graph_key(ctx, chunk, par, fold)] = en;
+  return SPX_OK;
+}
+// The graph for the current state (built when missing).
+int build_graph(spx_ctx* ctx, int chunk) {
+  return build_graph_for(ctx, chunk, ctx->wpar, ctx->last_fold);
+}
+// Every state's graph of `chunk`, so none is captured inside a timed region
+// (whatever windows were launched directly before it).
+int build_graphs_all(spx_ctx* ctx, int chunk) {
+  if (!ctx->win_k) return build_graph(ctx, chunk);  // (single pivots: no window state)
+  for (int par = 0; par < 2; ++par)
+    for (int f = 0; f < (ctx->fold || ctx->last_fold ? 2 : 1); ++f)
+      if (const int rc = build_graph_for(ctx, chunk, par, f != 0)) return rc;
+  return SPX_OK;
+}
+// Replay the graph of `chunk` for the current state and advance the state.
+int launch_graph(spx_ctx* ctx, int chunk) {
+  if (const int rc = build_graph(ctx, chunk)) return rc;
+  const auto& en = ctx->graphs[graph_key(ctx, chunk, ctx->wpar, ctx->last_fold)];
+  HIPC(hipGraphLaunch(en.exec, ctx->stream));
+  ctx->wpar = en.par_after;
+  ctx->last_fold = en.fold_after;
   return SPX_OK;
 }
 
@@ -1232,10 +1356,10 @@ int notres_resume(spx_ctx* ctx, int64_t fc, int64_t fr, int* retries) {
     return SPX_E_STATE;
   }
   uint32_t e = 0;
-  HIPC(hipMemcpyAsync(&e, ctx->win.epoch, sizeof(e), hipMemcpyDeviceToHost, ctx->stream));
+  HIPC(hipMemcpyAsync(&e, ctx->wins[0].epoch, sizeof(e), hipMemcpyDeviceToHost, ctx->stream));
   HIPC(hipStreamSynchronize(ctx->stream));
   e = (e + 1u) & TAG_EPOCH;
-  HIPC(hipMemcpyAsync(ctx->win.epoch, &e, sizeof(e), hipMemcpyHostToDevice, ctx->stream));
+  HIPC(hipMemcpyAsync(ctx->wins[0].epoch, &e, sizeof(e), hipMemcpyHostToDevice, ctx->stream));
   if (lazy_ok && !ctx->chain_denied) {
     ctx->chain_denied = true;
     drop_graphs(ctx);
@@ -1251,6 +1375,9 @@ int notres_resume(spx_ctx* ctx, int64_t fc, int64_t fr, int* retries) {
 // chain (a peer-only shard: the persistent chain again), as spx_solve's own
 // rerun does, so the request ends where it would have.
 int rp_recover(spx_ctx* ctx) {
+  // (every reader of the tableau comes through here: no leaving-row fix of a
+  // fold window may still be owed, whatever call left it)
+  if (const int rc = settle_fold(ctx)) return rc;
   if (ctx->rp_target < 0) return SPX_OK;
   const int64_t target = ctx->rp_target;
   ctx->rp_target = -1;
@@ -1269,6 +1396,7 @@ int rp_recover(spx_ctx* ctx) {
       rc = enqueue_pivots(ctx, n, 0);
       left -= n;
     }
+    if (!rc) rc = settle_fold(ctx);
     if (rc) return rc;
   }
 }
@@ -1303,24 +1431,40 @@ int alloc_common(spx_ctx* ctx, int64_t m_local, int64_t N, int64_t m_global, int
   HIPC(hipMalloc(&ctx->enter_part, sizeof(Key) * enter_part_len(ctx)));  // per wave / chain block
   HIPC(hipMalloc(&ctx->ratio_part, sizeof(Key) * ratio_part_len(ctx)));
   {
-    HIPC(hipMalloc(&ctx->win.F, sizeof(double) * KW * ctx->ld));
-    HIPC(hipMalloc(&ctx->win.P, sizeof(double) * KW * N));
-    HIPC(hipMalloc(&ctx->win.r, sizeof(int64_t) * KW));
-    HIPC(hipMalloc(&ctx->win.c, sizeof(int64_t) * KW));
-    HIPC(hipMalloc(&ctx->win.made, sizeof(int32_t) * KW));
-    HIPC(hipMalloc(&ctx->win.tag, sizeof(uint32_t) * N));
-    HIPC(hipMalloc(&ctx->win.epoch, sizeof(uint32_t)));
-    HIPC(hipMalloc(&ctx->win.nlist, sizeof(int32_t)));
-    HIPC(hipMalloc(&ctx->win.rec, sizeof(double) * RECW * N));
-    HIPC(hipMemsetAsync(ctx->win.nlist, 0, sizeof(int32_t), ctx->stream));
-    HIPC(hipMemsetAsync(ctx->win.rec, 0, sizeof(double) * RECW * N, ctx->stream));
-    HIPC(hipMemsetAsync(ctx->win.F, 0, sizeof(double) * KW * ctx->ld, ctx->stream));
-    HIPC(hipMemsetAsync(ctx->win.P, 0, sizeof(double) * KW * N, ctx->stream));
-    HIPC(hipMemsetAsync(ctx->win.made, 0, sizeof(int32_t) * KW, ctx->stream));
-    HIPC(hipMemsetAsync(ctx->win.r, 0, sizeof(int64_t) * KW, ctx->stream));
-    HIPC(hipMemsetAsync(ctx->win.c, 0, sizeof(int64_t) * KW, ctx->stream));
-    HIPC(hipMemsetAsync(ctx->win.tag, 0, sizeof(uint32_t) * N, ctx->stream));
-    HIPC(hipMemsetAsync(ctx->win.epoch, 0, sizeof(uint32_t), ctx->stream));
+    // shared by both window sets: column tags, the window epoch, the fold words
+    HIPC(hipMalloc(&ctx->wins[0].tag, sizeof(uint32_t) * N));
+    HIPC(hipMalloc(&ctx->wins[0].epoch, sizeof(uint32_t)));
+    HIPC(hipMalloc(&ctx->wins[0].fix, sizeof(int32_t) * 8));
+    HIPC(hipMemsetAsync(ctx->wins[0].tag, 0, sizeof(uint32_t) * N, ctx->stream));
+    HIPC(hipMemsetAsync(ctx->wins[0].epoch, 0, sizeof(uint32_t), ctx->stream));
+    HIPC(hipMemsetAsync(ctx->wins[0].fix, 0, sizeof(int32_t) * 8, ctx->stream));
+    for (int x = 0; x < 2; ++x) {
+      Window& w = ctx->wins[x];
+      w.tag = ctx->wins[0].tag;
+      w.epoch = ctx->wins[0].epoch;
+      w.fix = ctx->wins[0].fix;
+      w.sid = x;
+      HIPC(hipMalloc(&w.F, sizeof(double) * KW * ctx->ld));
+      HIPC(hipMalloc(&w.P, sizeof(double) * KW * N));
+      HIPC(hipMalloc(&w.r, sizeof(int64_t) * KW));
+      HIPC(hipMalloc(&w.c, sizeof(int64_t) * KW));
+      HIPC(hipMalloc(&w.made, sizeof(int32_t) * KW));
+      HIPC(hipMalloc(&w.nlist, sizeof(int32_t)));
+      HIPC(hipMalloc(&w.rec, sizeof(double) * RECW * N));
+      HIPC(hipMalloc(&w.frt, sizeof(double) * KW * KW));
+      HIPC(hipMalloc(&w.Pf, sizeof(double) * KW * N));
+      HIPC(hipMemsetAsync(w.Pf, 0, sizeof(double) * KW * N, ctx->stream));
+      HIPC(hipMemsetAsync(w.frt, 0, sizeof(double) * KW * KW, ctx->stream));
+      HIPC(hipMemsetAsync(w.nlist, 0, sizeof(int32_t), ctx->stream));
+      HIPC(hipMemsetAsync(w.rec, 0, sizeof(double) * RECW * N, ctx->stream));
+      HIPC(hipMemsetAsync(w.F, 0, sizeof(double) * KW * ctx->ld, ctx->stream));
+      HIPC(hipMemsetAsync(w.P, 0, sizeof(double) * KW * N, ctx->stream));
+      HIPC(hipMemsetAsync(w.made, 0, sizeof(int32_t) * KW, ctx->stream));
+      HIPC(hipMemsetAsync(w.r, 0, sizeof(int64_t) * KW, ctx->stream));
+      HIPC(hipMemsetAsync(w.c, 0, sizeof(int64_t) * KW, ctx->stream));
+    }
+    ctx->wpar = 0;
+    ctx->last_fold = false;
     const size_t ge = sizeof(unsigned long long) * ENTER_REC * CHAIN_MAX_BLOCKS;
     // shards: every rank's records, two parity halves and the window-end plane
     // (peers write them over xGMI: uncached, so this GPU's L2 never serves a
@@ -1412,6 +1556,8 @@ int spx_create(spx_ctx** out, int device) {
   // windows per replayed graph (1..16; tuning hook)
   if (const char* gw = std::getenv("SPX_GRAPH_WINDOWS"))
     ctx->graph_windows = std::max(1, std::min(16, std::atoi(gw)));
+  // the row_fix fold (A/B hook): SPX_ROW_FIX_FOLD=0 off
+  if (const char* f = std::getenv("SPX_ROW_FIX_FOLD")) ctx->fold = std::atoi(f) != 0;
   *out = ctx;
   return SPX_OK;
 }
@@ -1599,7 +1745,8 @@ int spx_peer_export(spx_ctx* ctx, void* out, int64_t cap) {
   HIPC(hipSetDevice(ctx->device));
   HIPC(hipIpcGetMemHandle(&b.hA, ctx->A));
   HIPC(hipIpcGetMemHandle(&b.hR, ctx->gr_ratio));
-  ctx->exported = true;
+  ctx->ever_exported.insert(ctx->A);
+  ctx->ever_exported.insert(ctx->gr_ratio);
   b.ld = ctx->ld;
   b.row0 = ctx->row0;
   b.m_local = ctx->m_local;
@@ -1674,6 +1821,7 @@ int spx_peer_import(spx_ctx* ctx, const void* blobs, int nranks) {
   }
   if ((rc = peer_commit(ctx, pe, B, cb))) return rc;
   ctx->peer_gen++;  // (every rank imports together: the same generation everywhere)
+  ctx->imported_load = true;
   return SPX_OK;
 }
 
@@ -1747,15 +1895,22 @@ int spx_destroy(spx_ctx* ctx) {
     while (ctx->adm_calls > 0) adm_release_locked(a, ctx);  // (error paths)
   }
   if (ctx->adm_ev) (void)hipEventDestroy(ctx->adm_ev);
-  // the peers' release marks (close_peers) for this context's exported
-  // buffers, a bounded wait, then every buffer goes
-  const bool was_exported = ctx->exported || !ctx->pool.empty();
-  close_peers(ctx);
-  if (was_exported && ctx->peer_gen > 0) (void)wait_peer_release(ctx, 10.0);
-  ctx->exported = false;
+  // the peers' release marks (close_peers) for every record buffer this
+  // context exported that peers imported -- the current one if this load was
+  // imported, and each pooled one under the generation it was imported with
+  // (a reload without a re-import has no marks to wait for in the
+  // current buffer) -- within one bounded wait, then every buffer goes
+  free_buffers(ctx);  // (closes this context's mappings of its peers; the
+                      // current exported buffers join the pool, with their generation)
+  {
+    const auto deadline = std::chrono::steady_clock::now() + std::chrono::seconds(10);
+    for (const auto& e : ctx->pool)
+      if (e.role == POOL_RECORDS && e.gen > 0)
+        (void)wait_peer_release(ctx, static_cast<const unsigned long long*>(e.p), e.gen, deadline);
+  }
   for (const auto& e : ctx->pool) (void)hipFree(e.p);
   ctx->pool.clear();
-  free_buffers(ctx);
+  ctx->ever_exported.clear();
   for (auto* pool : {&ctx->ev, &ctx->evc})
     for (auto& e : *pool) {
       (void)hipEventDestroy(e.first);
@@ -1833,8 +1988,8 @@ int spx_load_rows(spx_ctx* ctx, const double* A, int64_t m_local, int64_t cols, 
   int rc = alloc_common(ctx, m_local, cols, m_global, row0);
   if (rc) return rc;
   if (m_local > 0) {
-    // the column padding rows (ld > m_local) hold zeros, whatever the buffer held
-    if (ctx->ld > m_local) HIPC(hipMemsetAsync(ctx->A, 0, ctx->A_bytes, ctx->stream));
+    // (the column padding rows, ld > m_local, hold zeros: alloc_common cleared
+    // the ld * N doubles, whatever a pooled buffer held)
     if (layout == SPX_COL_MAJOR) {
       HIPC(hipMemcpy2DAsync(ctx->A, sizeof(double) * ctx->ld, A, sizeof(double) * ld,
                             sizeof(double) * m_local, cols, hipMemcpyHostToDevice,
@@ -1980,7 +2135,7 @@ int spx_solve(spx_ctx* ctx, const spx_opts* opts, spx_result* res) {
       ctx->win_k ? ctx->win_k * ctx->graph_windows : (o->chunk > 0 ? o->chunk : 32);
   const bool use_graph = o->use_graph != 0 && !ctx->loop && !ctx->time_chain;
   if (use_graph) {
-    rc = build_graph(ctx, chunk);
+    rc = build_graphs_all(ctx, chunk);
     if (rc) return rc;
   }
   int status = SPX_RUNNING;
@@ -1990,7 +2145,8 @@ int spx_solve(spx_ctx* ctx, const spx_opts* opts, spx_result* res) {
   // launches: every kernel checks the device status first.
   auto launch_chunk = [&](int64_t i) -> int {
     if (use_graph) {
-      HIPC(hipGraphLaunch(ctx->gexec, ctx->stream));
+      const int r = launch_graph(ctx, chunk);
+      if (r) return r;
     } else {
       const int r = enqueue_pivots(ctx, chunk, 0);
       if (r) return r;
@@ -2028,6 +2184,7 @@ int spx_solve(spx_ctx* ctx, const spx_opts* opts, spx_result* res) {
       if (ctx->rank == 0 && ctx->h_stop) __atomic_store_n(ctx->h_stop, 1, __ATOMIC_SEQ_CST);
     }
   }
+  if ((rc = settle_fold(ctx))) return rc;  // the last window's leaving rows
   if ((rc = pull_state(ctx))) return rc;  // the final state (after the extra chunk)
   adm_call.drained = true;
   if (status < 0 || is_fault(ctx->h_st->status)) return fault(ctx);
@@ -2053,7 +2210,7 @@ int spx_pivot(spx_ctx* ctx, const spx_opts* opts, int64_t* r, int64_t* c) {
   if (rc) return rc;
   const int64_t it0 = ctx->h_st->iters;
   for (int retries = 0;;) {
-    if ((rc = enqueue_pivots(ctx, 1, 0))) return rc;
+    if ((rc = enqueue_pivots(ctx, 1, 0)) || (rc = settle_fold(ctx))) return rc;
     if ((rc = pull_state(ctx))) return rc;
     if (ctx->h_st->status != ST_NOTRES) break;
     if ((rc = notres_resume(ctx, -1, -1, &retries))) return rc;
@@ -2080,7 +2237,7 @@ int spx_pivot_at(spx_ctx* ctx, int64_t r, int64_t c) {
   if (rc) return rc;
   // (pull the post-pivot state before writing the forced fields back)
   for (int retries = 0;;) {
-    if ((rc = enqueue_pivots(ctx, 1, 0))) return rc;
+    if ((rc = enqueue_pivots(ctx, 1, 0)) || (rc = settle_fold(ctx))) return rc;
     if ((rc = pull_state(ctx))) return rc;
     if (ctx->h_st->status != ST_NOTRES) break;
     if ((rc = notres_resume(ctx, c, r, &retries))) return rc;
@@ -2123,19 +2280,23 @@ int spx_run_pivots(spx_ctx* ctx, const spx_opts* opts, int64_t npivots, int time
     // between two stream events; the untimed windows replay graphs (below).
     // (One graph of the whole request ran 18 % slower at config 3: a hipGraph
     // of ~550 nodes is submitted in batches the GPU overtakes.)
-    if (!ctx->win_k || !graph) return enqueue_all(time_elim);
+    if (!ctx->win_k || !graph) {
+      rc = enqueue_all(time_elim);
+      return rc ? rc : settle_fold(ctx);
+    }
     // the untimed windows between two timed ones replay the graph of
-    // graph_windows windows (the one an untimed call builds, so no graph is
-    // captured inside a timed region); shorter runs are launched directly
+    // graph_windows windows (the ones an untimed call builds, for every
+    // window state, so no graph is captured inside a timed region); shorter
+    // runs are launched directly
     const int run = ctx->graph_windows;
-    if (time_elim > run && (rc = build_graph(ctx, run * ctx->win_k))) return rc;
+    if (time_elim > run && (rc = build_graphs_all(ctx, run * ctx->win_k))) return rc;
     int64_t done = 0;
     for (int64_t w = 0; done < npivots;) {
       const int n = (int)std::min<int64_t>(ctx->win_k, npivots - done);
       const bool timed = w % time_elim == 0;
       if (!timed && time_elim > run && npivots - done >= (int64_t)run * ctx->win_k &&
           (w % time_elim) + run <= time_elim) {
-        HIPC(hipGraphLaunch(ctx->gexec, ctx->stream));
+        if ((rc = launch_graph(ctx, run * ctx->win_k))) return rc;
         done += (int64_t)run * ctx->win_k;
         w += run;
         continue;
@@ -2144,18 +2305,20 @@ int spx_run_pivots(spx_ctx* ctx, const spx_opts* opts, int64_t npivots, int time
       done += n;
       ++w;
     }
-    return SPX_OK;
+    return settle_fold(ctx);
   }
   if (!time_elim && graph) {
     const int chunk =
         ctx->win_k ? ctx->win_k * ctx->graph_windows : (o->chunk > 0 ? o->chunk : 32);
-    if ((rc = build_graph(ctx, chunk))) return rc;
+    if ((rc = build_graphs_all(ctx, chunk))) return rc;
     int64_t left = npivots;
-    for (; left >= chunk; left -= chunk) HIPC(hipGraphLaunch(ctx->gexec, ctx->stream));
-    if (left > 0) return enqueue_pivots(ctx, (int)left, 0);
-    return SPX_OK;
+    for (; left >= chunk; left -= chunk)
+      if ((rc = launch_graph(ctx, chunk))) return rc;
+    if (left > 0 && (rc = enqueue_pivots(ctx, (int)left, 0))) return rc;
+    return settle_fold(ctx);
   }
-  return enqueue_all(time_elim);
+  rc = enqueue_all(time_elim);
+  return rc ? rc : settle_fold(ctx);
 }
 
 // Windowed (delayed) elimination: K pivots per tableau pass (2..16), 0/1 = off.
@@ -2199,7 +2362,22 @@ int spx_set_window(spx_ctx* ctx, int K) {
   CHECK_ARG(K == 0 || K == 1 || K == 2 || K == 4 || K == 8 || K == 12 || K == 16 || K == 24 || K == 28 ||
                 K == 32,
             "window must be 0, 1, 2, 4, 8, 12, 16, 24, 28 or 32");
+  if (const int rc = settle_fold(ctx)) return rc;  // (its gated row_fix is of the old K)
   ctx->win_k = K <= 1 ? 0 : K;
+  drop_graphs(ctx);
+  return SPX_OK;
+}
+
+// The row_fix fold: 1 the persistent single-GPU chain
+// rewrites the previous window's leaving rows, 0 (default) a row_fix launch
+// after every window.  Bit-identical either way; measured no faster (the fix
+// moves onto the chain's critical path), so off.  SPX_ROW_FIX_FOLD=1 sets 1 at
+// create (A/B runs).
+int spx_set_row_fix_fold(spx_ctx* ctx, int on) {
+  if (!ctx) return SPX_E_ARG;
+  CHECK_ARG(on == 0 || on == 1, "row_fix fold must be 0 or 1");
+  if (const int rc = settle_fold(ctx)) return rc;
+  ctx->fold = on;
   drop_graphs(ctx);
   return SPX_OK;
 }
@@ -2422,6 +2600,8 @@ int spx_chain_shm_path(int device, char* out, int cap) {
 // persistent window abort at its start, so the call reruns it (test hook).
 int spx_set_chain_handshake(spx_ctx* ctx, int64_t us) {
   if (!ctx) return SPX_E_ARG;
+  // (-k: abort every k-th window; k must fit the device's 32-bit modulo)
+  CHECK_ARG(us >= -(int64_t)INT32_MAX && us <= (int64_t)1 << 40, "handshake bound out of range");
   ctx->hs_us = us;
   return SPX_OK;
 }
@@ -2464,6 +2644,24 @@ int spx_peer_debug(spx_ctx* ctx, uint64_t* out, int n) {
     out[3 + 2 * q] = ctx->peer_ok ? (uint64_t)(uintptr_t)ctx->peers.A[q] : 0;
     out[4 + 2 * q] = ctx->peer_ok ? (uint64_t)(uintptr_t)ctx->peers.ratio[q] : 0;
   }
+  return SPX_OK;
+}
+
+// Diagnostic: out[0] buffers this context ever exported, out[1]
+// buffers in its pool, out[2] ever-exported buffers still held (pooled or the
+// current load's): out[0] == out[2] while none was freed.  n >= 3.
+int spx_peer_pool_debug(spx_ctx* ctx, uint64_t* out, int n) {
+  if (!ctx || !out) return SPX_E_ARG;
+  CHECK_ARG(n >= 3, "spx_peer_pool_debug: out too small");
+  uint64_t held = 0;
+  for (void* p : ctx->ever_exported) {
+    bool h = p == (void*)ctx->A || p == (void*)ctx->gr_ratio;
+    for (const auto& e : ctx->pool) h |= e.p == p;
+    held += h ? 1 : 0;
+  }
+  out[0] = ctx->ever_exported.size();
+  out[1] = ctx->pool.size();
+  out[2] = held;
   return SPX_OK;
 }
 

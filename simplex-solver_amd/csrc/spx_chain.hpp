@@ -672,15 +672,33 @@ __device__ __forceinline__ double sys_load(const double* p) {
 // written by the previous kernel (norm<INIT> or the previous window's chain);
 // the chain writes one partial per block there for the next window.
 // ---------------------------------------------------------------------------
-template <int KMAX, int CB>
+//
+// FOLD (round 6, the row_fix fold): the previous window's
+// leaving rows are rewritten by this launch instead of a row_fix launch after
+// its flush.  `pw` is that window's buffer set; if it owes its fix (pw.fix: G
+// set by its chain, no gated row_fix since), every thread first rewrites the
+// previous window's last-leaving rows r_L of ITS OWN column j when j took the
+// flush's fast path there (tag == that window's epoch, no flags): p_L[j], then
+// the later slots' msub with f_s[r_L] -- row_fix's arithmetic, from pw.Pf (the
+// p history, slot-major) and pw.frt (f_s[r_L]), both stored by that chain as
+// side stores of its slots.  The stores are write-through and drained before the
+// block's start-handshake arrival, so after the handshake every block reads
+// them: the norm phase gathers row r_q on the columns its thread rewrote
+// itself, and the ratio phase reads a rewritten row with coherent (sc1) loads.
+// This launch then owes its own fix (G[win.sid] = its epoch); the next fold
+// chain or a gated row_fix settles it.
+// ---------------------------------------------------------------------------
+template <int KMAX, int CB, bool FOLD = false>
 __global__ __launch_bounds__(CB) void chain_kernel(
     Key* __restrict__ enter_part, State* st, const Params* __restrict__ prm, int n_ep,
     const double* __restrict__ A, int64_t ld, int64_t m, int64_t N, double* __restrict__ obj,
     Window win, int npiv, int64_t* __restrict__ basis, int64_t* __restrict__ hist,
     unsigned long long* gr_enter_, unsigned long long* gr_ratio_, int cpb, int rpb,
-    const ChainPeers* __restrict__ /*pe: shards only*/) {
+    const ChainPeers* __restrict__ /*pe: shards only*/, Window pw = Window{}, int nfix = 0,
+    double* Aw = nullptr) {
   static_assert(KMAX <= 32, "slots are lane-indexed and fit the window buffers");
   constexpr int NW = CB / 64;
+  static_assert(!FOLD || KMAX * CB * 16 <= 128 * 1024, "the fold reads the LDS f histories");
   // LEAN (round 5; wherever the LDS histories allow it):
   // the slot chains carry no per-slot "s < q" select.  A slot s >= q is an exact identity instead: its f and p
   // histories are +0 (LDS zeroed at the window start, record lanes >= q are
@@ -717,6 +735,15 @@ __global__ __launch_bounds__(CB) void chain_kernel(
   const int w = t >> 6;
   const bool w0 = t < 64;
   const bool leader = b == 0 && t == 0;
+  SPX_PROBE(KMAX + 2, 0, 0, true);  // (probe build: the chain's entry)
+  // FOLD: does the previous window's set owe its fix (G set, no gated row_fix
+  // since)?  Nothing writes pw.fix during this launch.
+  int32_t fg = 0;
+  bool pend = false;
+  if constexpr (FOLD) {
+    fg = pw.fix[pw.sid];
+    pend = fg != 0 && fg != pw.fix[2 + pw.sid];
+  }
   // --- everything that does not depend on a pivot, in one batch ---
   const int32_t status0 = st->status;
   const int64_t forced_c = st->forced_c;
@@ -766,6 +793,73 @@ __global__ __launch_bounds__(CB) void chain_kernel(
   // per-thread slot masks (bit s): my row left at slot s (i == r_s), my column
   // entered at slot s (j == c_s), p_s[j] == 0 under the skip rule
   uint32_t rmask = 0u, cmask = 0u, zmask = 0u;
+  // FOLD: the previous window's leaving rows (lane s: r_s and whether s is
+  // the row's last leaving slot; xfr[L][s] = f_s[r_L] from pw.frt, in LDS)
+  // and my column's p history there (pw.Pf, slot-major) -- loaded with the
+  // kernel's first batch, whether or not a fix is owed (one round trip)
+  __shared__ double xfr[FOLD ? KMAX : 1][FOLD ? KMAX : 1];
+  int64_t xr = -1;
+  int xl = 0, xmk = 0;
+  if constexpr (FOLD) {
+    constexpr int PERT = (KMAX * KMAX + CB - 1) / CB;
+    double fv[PERT];
+#pragma unroll
+    for (int u = 0; u < PERT; ++u) {
+      const int x = t + CB * u;
+      fv[u] = x < KMAX * KMAX ? pw.frt[(x / KMAX) * KW + x % KMAX] : 0.0;
+    }
+    xr = lane < KMAX ? pw.r[lane] : -1;
+    const int pm = lane < KMAX ? pw.made[lane] : 0;
+    double pp[KMAX];
+#pragma unroll
+    for (int s2 = 0; s2 < KMAX; ++s2) pp[s2] = pw.Pf[(int64_t)s2 * N + jc];
+    // the RHS column's p history by lane (the wave of the last thread, when
+    // it keeps the RHS column beside its own: xown)
+    const bool xw = (int64_t)B * cpb == N - 1 && b == B - 1 && w == NW - 1;
+    const double prl = xw && lane < KMAX ? pw.Pf[(int64_t)lane * N + N - 1] : 0.0;
+    if (pend) {
+      const uint32_t fe = (uint32_t)fg & TAG_EPOCH;  // that window's epoch
+      const bool pfj = jlive && tg0 == fe;  // my column took its fast path there
+      xmk = __popcll(__ballot(pm != 0));  // (a prefix: its chain cleared the rest)
+      bool last = lane < xmk;
+#pragma unroll
+      for (int s2 = 1; s2 < KMAX; ++s2)
+        last &= !(s2 > lane && s2 < xmk && rdlane64(xr, s2) == xr);
+      xl = last ? 1 : 0;
+#pragma unroll
+      for (int u = 0; u < PERT; ++u) {
+        const int x = t + CB * u;
+        if (x < KMAX * KMAX) xfr[x / KMAX][x % KMAX] = fv[u];
+      }
+      __syncthreads();
+      // row_fix's value of (r_L, j) for each last-leaving slot L, stored
+      // write-through (wave-uniform L: one msub chain per lane)
+#pragma unroll
+      for (int L = 0; L < KMAX; ++L) {
+        if (!__builtin_amdgcn_readlane(xl, L)) continue;
+        const int64_t rL = rdlane64(xr, L);
+        double x = pp[L];
+#pragma unroll
+        for (int s2 = L + 1; s2 < KMAX; ++s2)
+          if (s2 < xmk) x = msub(x, xfr[L][s2], pp[s2]);
+        if (pfj) wt_store(const_cast<double*>(A) + jc * ld + rL, x);
+      }
+      // the RHS column (xown): its wave's lane L takes slot L
+      if (xw && (uint32_t)__builtin_amdgcn_readlane((int)tgx0, 63) == fe) {
+        const int L = lane < KMAX ? lane : 0;
+        double x = prl;
+#pragma unroll
+        for (int s2 = 1; s2 < KMAX; ++s2) {
+          const double p_s = rdlane(prl, s2);
+          if (s2 > L && s2 < xmk) x = msub(x, xfr[L][s2], p_s);
+        }
+        if (xl) wt_store(const_cast<double*>(A) + (N - 1) * ld + xr, x);
+      }
+      drain_stores();
+      __syncthreads();  // (every store of the block drained before its arrival)
+      SPX_PROBE(KMAX + 2, 0, 1, true);  // (probe build: the fold's rows stored)
+    }
+  }
   if (t == 0) lds_pin[b % PIN] = 0.0;
   SPX_PROBE_CHAIN_HW();
   if constexpr (LEAN) {  // slots s >= q read +0 histories (written at slot s only)
@@ -773,8 +867,11 @@ __global__ __launch_bounds__(CB) void chain_kernel(
     for (int s = 0; s < KMAX; ++s) fsl[s][t] = psl[s][t] = 0.0;
   }
   if (status0 != ST_RUNNING) {          // grid-uniform: no pivot in this window
-    if (leader)
-      for (int s = 0; s < npiv; ++s) win.made[s] = 0;  // (the flush counts made slots)
+    if (leader) {
+      // (the flush counts made slots; a fold set's made slots are exactly its pivots)
+      for (int s = 0; s < (FOLD ? KMAX : npiv); ++s) win.made[s] = 0;
+      if constexpr (FOLD) win.fix[win.sid] = 0;  // this window owes nothing
+    }
     return;
   }
   {
@@ -792,9 +889,24 @@ __global__ __launch_bounds__(CB) void chain_kernel(
     if (hs_res != 0) {  // (2: ST_FAULT is stored already)
       if (leader) {
         if (hs_res == 1) st->status = ST_NOTRES;
-        for (int s = 0; s < npiv; ++s) win.made[s] = 0;
+        for (int s = 0; s < (FOLD ? KMAX : npiv); ++s) win.made[s] = 0;
+        if constexpr (FOLD) win.fix[win.sid] = 0;
       }
       return;
+    }
+  }
+  SPX_PROBE(KMAX + 2, 0, 2, true);  // (probe build: the handshake passed)
+  // FOLD: does my row hold a rewritten value (it left the previous window)?
+  // Then column reads of it are coherent (sc1) loads: another block rewrote it
+  bool dirty = false, wdirty = false;
+  if constexpr (FOLD) {
+    if (pend) {
+#pragma unroll
+      for (int s2 = 0; s2 < KMAX; ++s2)
+        dirty |= __builtin_amdgcn_readlane(xl, s2) && rdlane64(xr, s2) == i;
+      dirty = dirty && ilive;
+      wdirty = __ballot(dirty) != 0ull;
+      if (wdirty && dirty) bcur = wt_load(A + (N - 1) * ld + ic);
     }
   }
   if (leader) {
@@ -852,6 +964,9 @@ __global__ __launch_bounds__(CB) void chain_kernel(
     // column c on my row: stale + pending slots, in slot order; p_s[c] (lane
     // s) from the winning entering record's history
     double fv = A[c * ld + ic];
+    if constexpr (FOLD) {  // (a row another block rewrote at the window start)
+      if (wdirty && dirty) fv = wt_load(A + c * ld + ic);
+    }
     if constexpr (LH) {  // my row's f history, read while the gathers are in flight
 #pragma unroll
       for (int s = 0; s < KMAX; ++s) fs[s] = fsl[s][t];
@@ -965,6 +1080,11 @@ __global__ __launch_bounds__(CB) void chain_kernel(
     // f_q for the flush / row_fix (later kernels): stored after the record, so
     // these stores never queue in front of it
     if (ilive) win.F[(int64_t)q * ld + i] = fv;
+    if constexpr (FOLD) {
+      // my row left earlier in this window (last at slot L): f_q of it, for
+      // the next fold chain's rewrite of the row (win.frt[L][q])
+      if (ilive && rmask != 0u) win.frt[(31 - __builtin_clz(rmask)) * KW + q] = fv;
+    }
     SPX_PROBE(q, 0, 3, true);
     // ================= norm phase q =================
     SPX_PROBE(q, 1, 0, true);
@@ -1143,6 +1263,17 @@ __global__ __launch_bounds__(CB) void chain_kernel(
       SPX_PROBE_CHAIN(q, 2);
     }
     // stores for later kernels, after the record (never queued in front of it):
+    if constexpr (FOLD) {
+      // p_q by column, slot-major (win.Pf), for the next fold chain; the
+      // polling wave's columns are stored by the last wave (from LDS: psl is
+      // complete after the barrier above), so the poller issues no stores
+      if (w > 0 && jlive) win.Pf[(int64_t)q * N + j] = pq;
+      if (w == NW - 1) {
+        const int64_t j0 = (int64_t)b * cpb + lane;
+        if (lane < cpb && j0 < N) win.Pf[(int64_t)q * N + j0] = psl[q][lane];
+      }
+      if (xown) win.Pf[(int64_t)q * N + N - 1] = prhs;
+    }
     // the pivot's bookkeeping (the flush and row_fix read p from the records)
     if (b == 0 && t == CB - 1) {  // block 0's last thread: not in the polling wave
       st->r = r;
@@ -1166,6 +1297,15 @@ __global__ __launch_bounds__(CB) void chain_kernel(
     st->status = stop_status;
     if (stop_status == ST_OPTIMAL) st->c_next = -1;
     for (int s = q; s < npiv; ++s) win.made[s] = 0;
+  }
+  if constexpr (FOLD) {
+    if (leader) {
+      // a fold set's made slots are exactly its pivots (the next fold chain
+      // counts them), and it owes its leaving rows' fix: G = its epoch
+      // (bit 30 set, never 0)
+      for (int s = q; s < KMAX; ++s) win.made[s] = 0;
+      win.fix[win.sid] = q > 0 ? (int32_t)(W | 0x40000000u) : 0;
+    }
   }
   if (jlive) {
     obj[j] = o;
@@ -1235,7 +1375,8 @@ __global__ __launch_bounds__(CB) void chain_shard_kernel(
     const double* __restrict__ A, int64_t ld, int64_t m, int64_t N, double* __restrict__ obj,
     Window win, int npiv, int64_t* __restrict__ basis, int64_t* __restrict__ hist,
     unsigned long long* gr_enter_, unsigned long long* gr_ratio_, int cpb, int rpb,
-    const ChainPeers* __restrict__ pe) {
+    const ChainPeers* __restrict__ pe, Window /*pw: chain_kernel's fold only*/, int /*nfix*/,
+    double* /*Aw*/) {
   static_assert(KMAX <= 32, "slots are lane-indexed and fit the window buffers");
   constexpr int NW = CB / 64;
 

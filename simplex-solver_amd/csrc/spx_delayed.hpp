@@ -103,6 +103,18 @@ struct Window {
   int32_t* nlist;    // 1             : records in `rec` (reset by lazy_ratio slot 0)
   double* rec;       // N x RECW      : the window's touched columns, compacted by the
                      //                 last lazy_norm: [j | path flags, pad, p_0 .. p_{K-1}]
+  // Two sets of the per-window buffers (F, P, r, c, made, nlist, rec) alternate
+  // by window (the host's parity), so a window's buffers outlive the next
+  // window's chain: the row_fix fold resolves window w-1's
+  // leaving rows inside window w's chain.  tag, epoch and fix are shared.
+  int32_t* fix;      // 5 words: [0..1] G: the window epoch whose leaving rows set s
+                     //   still owes (a fold chain's, 0: none); [2..3] Z: the epoch
+                     //   a gated row_fix resolved; [4] that kernel's block counter
+  int32_t sid;       // this set's index (0 / 1)
+  double* frt;       // KW x KW : frt[L*KW + s] = f_s[r_L] for a row whose last leaving
+                     //           slot is L (written by a fold chain, for the next one)
+  double* Pf;        // KW x N  : p_s[j] at Pf[s*N + j] (slot-major; a fold chain's, for
+                     //           the next one)
 };
 
 constexpr int RECW = KW + 2;  // doubles per record (272 B)
@@ -836,17 +848,19 @@ __global__ __launch_bounds__(BLK) void flush_lds_kernel(double* __restrict__ A, 
 // whose last leaving slot is L ends at p_L[j] followed by the later pivots'
 // msub updates (their leaving rows differ from r).  One thread per column.
 // ---------------------------------------------------------------------------
-template <int K, int TPB = BLK>
-__global__ __launch_bounds__(TPB) void row_fix_kernel(double* __restrict__ A, int64_t ld,
-                                                      int64_t m_local, int64_t row0, int64_t N,
-                                                      Window win, int npiv) {
+// fix_rows<K, TPB>: the body of row_fix_kernel -- the records kr0, kr0 +
+// stride, ... of `win`, one per thread at a time (the first loaded before the
+// list length is known); also run by the fold blocks of chain_kernel<.., true>
+// on the previous window's set (INCHAIN: no probe stamps).
+template <int K, int TPB, bool INCHAIN = false>
+__device__ __forceinline__ void fix_rows(double* A, int64_t ld, int64_t m_local, int64_t row0,
+                                         int64_t N, const Window& win, int npiv, int64_t kr0,
+                                         int64_t stride) {
   __shared__ double fr[K][K];  // fr[L][s] = f_s[r_L]
   __shared__ int64_t rows[K];
   __shared__ int lastL[K];
   __shared__ int made_sh[K];
   const int t = threadIdx.x;
-  SPX_PROBE(K + 1, 0, 0, true);
-  SPX_PROBE_RF_BLOCK(0);
   // one thread per record of the window (the flush's compacted list: column,
   // path flags, p_0..p_{K-1}).  Two rounds of dependent loads: (1) the record
   // (its index clamped to the buffer, not to the list length, so it does not
@@ -858,10 +872,10 @@ __global__ __launch_bounds__(TPB) void row_fix_kernel(double* __restrict__ A, in
   // and ~2.5 us to issue the scattered stores (the stores themselves: ~1.4
   // us).  64-thread blocks and the K chains interleaved slot-major measured
   // 14.3-14.9 us, not kept.)
-  const int kr = blockIdx.x * TPB + t;
-  const int64_t kc = kr < N ? kr : N - 1;  // the record buffer holds N records
+  int64_t kr = kr0;
+  int64_t kc = kr < N ? kr : N - 1;  // the record buffer holds N records
   const int nl = *win.nlist;
-  const int64_t hdr = reinterpret_cast<const int64_t*>(win.rec)[kc * RECW];
+  int64_t hdr = reinterpret_cast<const int64_t*>(win.rec)[kc * RECW];
   double p[K];
 #pragma unroll
   for (int s = 0; s < K; ++s) p[s] = win.rec[kc * RECW + 2 + s];
@@ -870,7 +884,7 @@ __global__ __launch_bounds__(TPB) void row_fix_kernel(double* __restrict__ A, in
     made_sh[t] = t < npiv ? win.made[t] : 0;
   }
   __syncthreads();
-  SPX_PROBE(K + 1, 0, 1, hdr != 12345 && p[K - 1] != 12345.678);  // round 1 arrived
+  if constexpr (!INCHAIN) SPX_PROBE(K + 1, 0, 1, hdr != 12345 && p[K - 1] != 12345.678);
   // made slots of this window: a prefix of its npiv launched ones
   int madeK = 0;
 #pragma unroll
@@ -898,21 +912,80 @@ __global__ __launch_bounds__(TPB) void row_fix_kernel(double* __restrict__ A, in
     const int x = t + u * TPB;
     if (x < K * K) fr[x / K][x % K] = fv[u];
   }
-  SPX_PROBE(K + 1, 0, 2, fv[0] != 12345.678);  // round 2 arrived
+  if constexpr (!INCHAIN) SPX_PROBE(K + 1, 0, 2, fv[0] != 12345.678);  // round 2 arrived
   __syncthreads();
-  SPX_PROBE(K + 1, 1, 2, true);  // lastL and the barrier done
-  const int64_t j = hdr & 0xffffffffll;
-  const bool fast = (hdr >> 32) == 0;  // not SPECIAL / ZERO: the flush's plain msub chain
-  if (madeK == 0 || kr >= nl || !fast) return;
+  if constexpr (!INCHAIN) SPX_PROBE(K + 1, 1, 2, true);  // lastL and the barrier done
+  if (madeK == 0) return;
+#pragma unroll 1
+  while (kr < nl) {
+    const int64_t j = hdr & 0xffffffffll;
+    const bool fast = (hdr >> 32) == 0;  // not SPECIAL / ZERO: the flush's plain msub chain
+    // (an opaque 0 in the LDS indices: the loop-invariant fr / rows / lastL
+    // reads would otherwise be hoisted out of the record loop, K^2 values
+    // held in registers)
+    int z = 0;
+    asm volatile("" : "+v"(z));
+    const double* frz = &fr[0][0] + z;
+    if (fast) {
 #pragma unroll
-  for (int L = 0; L < K; ++L) {
-    if (L >= madeK || !lastL[L] || rows[L] < 0 || rows[L] >= m_local) continue;  // not ours
-    double x = p[L];  // p_L[j], then the later slots
+      for (int L = 0; L < K; ++L) {
+        const int64_t rL = rows[L + z];
+        if (L >= madeK || !lastL[L + z] || rL < 0 || rL >= m_local) continue;  // not ours
+        double x = p[L];  // p_L[j], then the later slots
 #pragma unroll
-    for (int s = L + 1; s < K; ++s)
-      if (s < madeK) x = msub(x, fr[L][s], p[s]);
-    __builtin_nontemporal_store(x, A + j * ld + rows[L]);  // scattered 8-B writes: no L2 allocate
+        for (int s = L + 1; s < K; ++s)
+          if (s < madeK) x = msub(x, frz[L * K + s], p[s]);
+        __builtin_nontemporal_store(x, A + j * ld + rL);  // scattered 8-B writes: no L2 allocate
+      }
+    }
+    kr += stride;
+    if (kr >= nl) break;
+    hdr = reinterpret_cast<const int64_t*>(win.rec)[kr * RECW];
+#pragma unroll
+    for (int s = 0; s < K; ++s) p[s] = win.rec[kr * RECW + 2 + s];
   }
+}
+
+// ---------------------------------------------------------------------------
+// row_fix_kernel<K>: after a window's flush (its made slots: a prefix of K),
+// rewrite the leaving rows of the fast-path columns (the window's records
+// without SPECIAL / ZERO flags; p values from the records).  For such a column no
+// pivot of the window enters it and every p_s[j] != 0, so a leaving row r
+// whose last leaving slot is L ends at p_L[j] followed by the later pivots'
+// msub updates (their leaving rows differ from r).  One thread per column.
+// ---------------------------------------------------------------------------
+template <int K, int TPB = BLK, bool GATED = false>
+__global__ __launch_bounds__(TPB) void row_fix_kernel(double* __restrict__ A, int64_t ld,
+                                                      int64_t m_local, int64_t row0, int64_t N,
+                                                      Window win, int npiv) {
+  const int t = threadIdx.x;
+  SPX_PROBE(K + 1, 0, 0, true);
+  SPX_PROBE_RF_BLOCK(0);
+  // GATED (the row_fix fold, DESIGN.md §4b: after the last fold window of a
+  // call, or before a window that is not one): this set's leaving rows are
+  // rewritten only if a fold chain left them owed (G) and no gated row_fix
+  // resolved them since (Z); the last block to pass the gate records Z, so no
+  // block of this launch sees its own mark.  Ungated (every window of the
+  // launch-per-phase and row-sharded paths): always, and the set owes nothing
+  // afterwards (G = 0: nothing of it can be owed to a later fold chain).
+  if constexpr (GATED) {
+    __shared__ int pend_sh;
+    if (t == 0) {
+      const int32_t g = win.fix[win.sid], z = win.fix[2 + win.sid];
+      pend_sh = g != 0 && g != z;
+      __threadfence();
+      if (atomicAdd(&win.fix[4], 1) == (int)gridDim.x - 1) {
+        win.fix[2 + win.sid] = g;
+        win.fix[4] = 0;
+      }
+    }
+    __syncthreads();
+    if (!pend_sh) return;
+  } else {
+    if (blockIdx.x == 0 && t == 0) win.fix[win.sid] = 0;
+  }
+  fix_rows<K, TPB>(A, ld, m_local, row0, N, win, npiv, (int64_t)blockIdx.x * TPB + t,
+                   (int64_t)gridDim.x * TPB);
 #ifdef SPX_PHASE_TIMING
   SPX_PROBE(K + 1, 0, 3, true);  // stores issued
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");

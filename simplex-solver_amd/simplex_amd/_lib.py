@@ -98,6 +98,7 @@ SIGNATURES = {
     "spx_elim_timing": (ctypes.c_int, [_P, _DP, _LP, _LP, ctypes.c_int]),
     "spx_set_ld_pad": (ctypes.c_int, [_P, ctypes.c_int]),
     "spx_set_window": (ctypes.c_int, [_P, ctypes.c_int]),
+    "spx_set_row_fix_fold": (ctypes.c_int, [_P, ctypes.c_int]),
     "spx_set_chain": (ctypes.c_int, [_P, ctypes.c_int, ctypes.c_int]),
     "spx_set_chain_timing": (ctypes.c_int, [_P, ctypes.c_int]),
     "spx_chain_timing": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_double),
@@ -113,6 +114,7 @@ SIGNATURES = {
     "spx_set_peer_push": (ctypes.c_int, [_P, ctypes.c_int]),
     "spx_get_peer_push": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_int)]),
     "spx_peer_debug": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_uint64), ctypes.c_int]),
+    "spx_peer_pool_debug": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_uint64), ctypes.c_int]),
     "spx_get_chain_stats": (ctypes.c_int, [_P, _LP]),
     "spx_set_chain_handshake": (ctypes.c_int, [_P, _I64]),
     "spx_chain_shm_path": (ctypes.c_int, [ctypes.c_int, ctypes.c_char_p, ctypes.c_int]),

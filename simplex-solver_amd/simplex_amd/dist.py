@@ -133,6 +133,14 @@ class ShardedTableau(DeviceTableau):
                 "peer_A": [out[3 + 2 * q] for q in range(self.world)],
                 "peer_records": [out[4 + 2 * q] for q in range(self.world)]}
 
+    def peer_pool_debug(self) -> dict:
+        """Diagnostic: buffers this context ever exported, buffers in its pool,
+        and the ever-exported ones it still holds (spx_peer_pool_debug; an
+        exported buffer is never freed before close, so held == exported)."""
+        out = (ctypes.c_uint64 * 3)()
+        self._check(self._lib.spx_peer_pool_debug(self._ctx, out, 3), "spx_peer_pool_debug")
+        return {"exported": out[0], "pooled": out[1], "held": out[2]}
+
     @classmethod
     def from_env(cls, device: int | None = None, group=None) -> "ShardedTableau":
         import torch.distributed as dist

@@ -306,6 +306,14 @@ class DeviceTableau:
         """Windowed elimination: K pivots per pass over the tableau (0/1 = off)."""
         self._check(self._lib.spx_set_window(self._ctx, int(K)), "spx_set_window")
 
+
+    def set_row_fix_fold(self, on: bool = True) -> None:
+        """The row_fix fold (spx_set_row_fix_fold): a window's
+        leaving rows are rewritten inside the next window's chain launch (on)
+        or by a row_fix launch after every window (off, the default: the fold
+        measured no faster)."""
+        self._check(self._lib.spx_set_row_fix_fold(self._ctx, 1 if on else 0),
+                    "spx_set_row_fix_fold")
     def set_chain(self, mode: int = 0, min_blocks: int = 0) -> None:
         """Pivot chain of a window: 0 = one persistent launch per window when
         the tableau fits (default), 1 = two launches per pivot (lazy kernels),

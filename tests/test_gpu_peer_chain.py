@@ -349,6 +349,11 @@ def _free_port():
      "--then", "1024x8000,512x2048,1024x8000", "--ipc-log"],
     ["--rows", "512", "--cols", "2048", "--window", "24", "--pivots", "101",
      "--then", "1024x8000,512x2048", "--push"],
+    # reloads that take pooled (once exported) buffers without a
+    # new import must pool them again, never free them; the destroy then
+    # waits for no release marks (it used to wait out its 10 s bound)
+    ["--rows", "512", "--cols", "2048", "--window", "24", "--pivots", "101",
+     "--then", "1024x8000", "--end-no-import", "512x2048,300x500,512x2048,1024x8000"],
     # peer-only shards have no launch-per-phase path: every 3rd window aborts
     # at its start handshake and reruns persistent -- 30+ isolated aborts in
     # one solve, more than the 16 CONSECUTIVE ones a rank gives up after
@@ -384,6 +389,12 @@ def test_peer_chain_two_processes_ipc(args):
         # aborted at the handshake until rank 1 arrived), then both finished
         drains = {int(k): float(v) for k, v in re.findall(r"rank (\d+): drain ([0-9.]+) s", out)}
         assert drains[0] > 0.3 and drains[1] < drains[0], drains
+    if "--end-no-import" in args:
+        assert "an exported buffer was freed" not in out
+        held = re.findall(r"exported (\d+) held (\d+)", out)
+        assert held and all(a_ == b_ for a_, b_ in held), held
+        closes = [float(x) for x in re.findall(r"rank \d+: destroy ([0-9.]+) s", out)]
+        assert len(closes) == 2 and max(closes) < 3.0, closes
 
 
 @pytest.mark.timeout(400)

@@ -1,0 +1,277 @@
+"""The drop-in user path, timed: ``SolverController(...).run()`` end to end.
+
+The reference's performance contract is on its user path, not on the pivot
+loop alone (/root/reference/tests/test_performance_load.py): 10 concurrent
+users solving its load LP with the average under 5 s (:43-100), 50 sequential
+users without degradation (:102-145).  Those shapes are restated here through
+this build's controller (``simplex_amd.controller``, the GPU pivot engine
+behind the ``simple_simplex`` API), without Flask (the routes are out of scope,
+SURVEY §2): every report must equal the one the reference's path gives on the
+same LP -- HiGHS for the answer, and the CPU oracle standing in for the
+unavailable ``simple_simplex`` for the tables (parity unpinned against
+``simple_simplex`` itself) -- and the reference's thresholds
+are asserted.
+
+``test_user_path_stage_times`` times the stages of one solve (the text API and
+standard form, context create / load, pivots and snapshots, table and HTML
+extraction, the answer, save_solution) for config 1, the reference's load LP
+and config 2, beside the same controller with the oracle in place of the GPU
+engine (the reference's CPU path on this host).  With SPX_USER_PATH_JSON set
+it writes the table there (profiles/r06/user_path.json).
+"""
+import json
+import os
+import threading
+import time
+from concurrent.futures import ThreadPoolExecutor, as_completed
+
+import numpy as np
+import pytest
+
+from oracle import simplex_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+# the reference's load LP (tests/test_performance_load.py:31-38: max 3x1 + 5x2,
+# x1 <= 4, 2x2 <= 12, 3x1 + 2x2 <= 18), as the /new form hands it to /solve
+WYNDOR = {"problema_definicion": {
+    "funcion_objetivo": {"type": "maximize", "coefficients": {"x1": 3.0, "x2": 5.0}},
+    "restricciones": [
+        {"coefficients": {"x1": 1.0, "x2": 0.0}, "operator": "<=", "rhs": 4.0},
+        {"coefficients": {"x1": 0.0, "x2": 2.0}, "operator": "<=", "rhs": 12.0},
+        {"coefficients": {"x1": 3.0, "x2": 2.0}, "operator": "<=", "rhs": 18.0}]}}
+
+# config 1: the reference's 3-variable case
+# (tests/test_visualization_integration.py:417-444: max 2x1 + 3x2 + 3x3,
+# x1 + x2 + x3 <= 10, 2x1 + x2 <= 15, x2 + 3x3 <= 30)
+CONFIG1 = {"problema_definicion": {
+    "funcion_objetivo": {"type": "maximize",
+                         "coefficients": {"x1": 2.0, "x2": 3.0, "x3": 3.0}},
+    "restricciones": [
+        {"coefficients": {"x1": 1.0, "x2": 1.0, "x3": 1.0}, "operator": "<=", "rhs": 10.0},
+        {"coefficients": {"x1": 2.0, "x2": 1.0, "x3": 0.0}, "operator": "<=", "rhs": 15.0},
+        {"coefficients": {"x1": 0.0, "x2": 1.0, "x3": 3.0}, "operator": "<=", "rhs": 30.0}]}}
+
+
+def config2_wrapper():
+    """BASELINE config 2 (1024 x 2048 dense LP, seed 20251207) as a /solve
+    wrapper: variable names sort lexicographically in the controller (:46), so
+    they are zero-padded to keep the generator's column order."""
+    from simplex_amd import synth
+    m, n, seed = 1024, 2048, 20251207
+    A, b, c = synth.lp_data("dense", m, n, seed)
+    names = [f"x{j:04d}" for j in range(n)]
+    return {"problema_definicion": {
+        "funcion_objetivo": {"type": "maximize",
+                             "coefficients": dict(zip(names, c.tolist()))},
+        "restricciones": [{"coefficients": dict(zip(names, A[i].tolist())), "operator": "<=",
+                           "rhs": float(b[i])} for i in range(m)]}}
+
+
+def oracle_optimize_json_format(tableau, maximize=None, **_):
+    """The reference's CPU tableau path on this host: the oracle (numpy, the
+    spec of DESIGN.md §2) in place of simple_simplex.optimize_json_format,
+    with the same pivotSteps shape and the same snapshot budget as the GPU
+    engine (phase 2 only: the LPs here are all-<= with b >= 0)."""
+    from simplex_amd.simple_simplex import HISTORY_CELL_BUDGET
+    if maximize is None:
+        maximize = bool(tableau.maximize_flag)
+    sf = O.standard_form(tableau.c, tableau.rows, bool(maximize))
+    assert sf["k"] == 0, "stand-in: phase-2 LPs only"
+    T, basis = sf["T"], sf["basis"]
+    budget = [HISTORY_CELL_BUDGET]
+    steps = []
+
+    def snap(r, c, T_):
+        e = {"step": len(steps), "pivotRowIndex": r, "pivotColIndex": c, "phase": 2,
+             "tableau": []}
+        if budget[0] >= T_.size:
+            e["tableau"] = T_.tolist()
+            budget[0] -= T_.size
+        steps.append(e)
+
+    snap(None, None, T)
+    st, _ = O.solve_tableau(T, basis, n_enter=sf["n"] + sf["m"], on_pivot=snap)
+    if steps and not steps[-1]["tableau"]:
+        steps[-1]["tableau"] = T.tolist()
+    return {"pivotSteps": steps, "status_code": st}
+
+
+class StageTimer:
+    """Inclusive wall time of the controller's stages (monkeypatched wrappers;
+    one solve at a time)."""
+
+    def __init__(self, monkeypatch):
+        self.mp = monkeypatch
+        self.t = {}
+
+    def wrap(self, obj, name, stage):
+        fn = getattr(obj, name)
+
+        def timed(*a, **kw):
+            t0 = time.perf_counter()
+            try:
+                return fn(*a, **kw)
+            finally:
+                self.t[stage] = self.t.get(stage, 0.0) + time.perf_counter() - t0
+        self.mp.setattr(obj, name, timed)
+
+    def take(self):
+        out, self.t = self.t, {}
+        return out
+
+
+@pytest.fixture
+def out_dir(tmp_path, monkeypatch):
+    from simplex_amd import storage
+    monkeypatch.setattr(storage, "OUTPUT_DIR", str(tmp_path))
+    return tmp_path
+
+
+def _expected_report(wrapper, monkeypatch):
+    """The reference path's report (HiGHS + the oracle's tables)."""
+    from simplex_amd import controller as C
+    with monkeypatch.context() as mp:
+        mp.setattr(C, "optimize_json_format", oracle_optimize_json_format)
+        return C.SolverController(wrapper, answer_engine="highs").run()
+
+
+def _same_report(rep, ref, engine):
+    a, b = rep["solucion_encontrada"], ref["solucion_encontrada"]
+    assert a["status"] == b["status"] == "Solucion Factible"
+    assert abs(a["valor_optimo_z"] - b["valor_optimo_z"]) <= 1e-9 * max(1.0, abs(b["valor_optimo_z"]))
+    if engine == "highs":  # the same answer engine: the same values
+        assert a["valor_optimo_z"] == b["valor_optimo_z"]
+    # the tables: the GPU engine's snapshots equal the oracle's (rounded to 4 dp
+    # by the controller, as the reference renders them, :354)
+    assert rep["tablas_intermedias"] == ref["tablas_intermedias"]
+    assert rep["visualizacion_gilp_html"] == ref["visualizacion_gilp_html"]
+
+
+@pytest.mark.timeout(120)
+@pytest.mark.parametrize("engine", ["highs", "gpu"])
+def test_ten_concurrent_users(out_dir, monkeypatch, engine):
+    """Reference tests/test_performance_load.py:43-100: 10 users at once, every
+    report right, average < 5 s."""
+    from simplex_amd.controller import SolverController
+    ref = _expected_report(WYNDOR, monkeypatch)
+    assert ref["solucion_encontrada"]["valor_optimo_z"] == pytest.approx(36.0, rel=1e-12)
+    times, errors, reports = [], [], []
+    lock = threading.Lock()
+
+    def user():
+        t0 = time.perf_counter()
+        rep = SolverController(WYNDOR, answer_engine=engine).run()
+        with lock:
+            times.append(time.perf_counter() - t0)
+            reports.append(rep)
+
+    with ThreadPoolExecutor(max_workers=10) as ex:
+        for f in as_completed([ex.submit(user) for _ in range(10)]):
+            try:
+                f.result()
+            except Exception as e:  # noqa: BLE001
+                errors.append(repr(e))
+    assert not errors, errors[:3]
+    assert len(reports) == 10 and all(r is not None for r in reports)
+    for rep in reports:
+        _same_report(rep, ref, engine)
+    avg = sum(times) / len(times)
+    print(f"\n10 concurrent users ({engine}): avg {avg * 1e3:.1f} ms, max {max(times) * 1e3:.1f} ms")
+    assert avg < 5.0
+    # one report file per solve (+1: the reference path's), names never collide
+    assert len(list(out_dir.iterdir())) == 11
+
+
+@pytest.mark.timeout(240)
+@pytest.mark.parametrize("engine", ["highs", "gpu"])
+def test_fifty_sequential_users(out_dir, monkeypatch, engine):
+    """Reference tests/test_performance_load.py:102-145: 50 solves one after
+    another, no degradation (last 10 within +50 % of the first 10)."""
+    from simplex_amd.controller import SolverController
+    ref = _expected_report(WYNDOR, monkeypatch)
+    times = []
+    for _ in range(50):
+        t0 = time.perf_counter()
+        rep = SolverController(WYNDOR, answer_engine=engine).run()
+        times.append(time.perf_counter() - t0)
+        _same_report(rep, ref, engine)
+    first, last = sum(times[:10]) / 10, sum(times[-10:]) / 10
+    deg = (last - first) / first * 100.0
+    print(f"\n50 sequential users ({engine}): first 10 {first * 1e3:.2f} ms, last 10 "
+          f"{last * 1e3:.2f} ms, degradation {deg:.1f} %")
+    assert deg < 50.0
+
+
+def _stage_run(wrapper, engine, path, monkeypatch, reps):
+    """Median per-stage times of `reps` solves of `wrapper` (path "gpu": this
+    build; "cpu": the same controller with the oracle in place of the GPU
+    engine)."""
+    from simplex_amd import controller as C
+    from simplex_amd import lp, simple_simplex
+    from simplex_amd.storage import StorageService
+    runs = []
+    with monkeypatch.context() as mp:
+        st = StageTimer(mp)
+        if path == "cpu":
+            mp.setattr(C, "optimize_json_format", oracle_optimize_json_format)
+        st.wrap(C.SolverController, "_prepare_model_for_scipy", "model for linprog")
+        st.wrap(C, "linprog", "answer: linprog (HiGHS)")
+        st.wrap(C, "gpu_linprog", "answer: GPU linprog")
+        st.wrap(C, "create_tableau", "text API (strings + parse)")
+        st.wrap(C, "add_constraint", "text API (strings + parse)")
+        st.wrap(C, "add_objective", "text API (strings + parse)")
+        st.wrap(C.SolverController, "_run_simple_simplex", "pivot engine (whole)")
+        st.wrap(simple_simplex, "build_standard_form", "standard form")
+        st.wrap(lp.DeviceTableau, "__init__", "context create")
+        st.wrap(lp.DeviceTableau, "load", "load (H2D)")
+        st.wrap(lp.DeviceTableau, "pivot", "pivots (one per call)")
+        st.wrap(lp.DeviceTableau, "solve", "pivots (windows)")
+        st.wrap(lp.DeviceTableau, "tableau", "snapshots (D2H)")
+        st.wrap(lp.DeviceTableau, "close", "context destroy")
+        st.wrap(C.SolverController, "_extract_tableaus_from_simple_simplex", "tables (4 dp)")
+        st.wrap(C.SolverController, "_tableau_to_html", "HTML")
+        st.wrap(StorageService, "save_solution", "save_solution")
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            rep = C.SolverController(wrapper, answer_engine=engine).run()
+            total = time.perf_counter() - t0
+            assert rep is not None and rep["solucion_encontrada"]["status"] == "Solucion Factible"
+            d = st.take()
+            d["run() total"] = total
+            runs.append(d)
+    keys = sorted({k for d in runs for k in d})
+    return {k: float(np.median([d.get(k, 0.0) for d in runs])) for k in keys}, rep
+
+
+@pytest.mark.timeout(600)
+def test_user_path_stage_times(out_dir, monkeypatch):
+    """Stage times of SolverController.run() (medians), GPU engine vs the
+    oracle standing in for simple_simplex, on config 1, the load LP and
+    config 2; the GPU path's reports equal the stand-in's."""
+    cases = [("config 1 (3 vars, test_visualization_integration.py:417-444)", CONFIG1, 20),
+             ("load LP (Wyndor, test_performance_load.py:31-38)", WYNDOR, 20),
+             ("config 2 (1024 x 2048 dense, text API)", config2_wrapper(), 2)]
+    out = []
+    for name, wrap, reps in cases:
+        row = {"workload": name}
+        reps_ = {}
+        for engine in ("highs", "gpu"):
+            t, rep = _stage_run(wrap, engine, "gpu", monkeypatch, reps)
+            row[f"gpu_engine/answer_{engine}"] = t
+            reps_[engine] = rep
+        t, ref = _stage_run(wrap, "highs", "cpu", monkeypatch, reps)
+        row["cpu_reference_path/answer_highs"] = t
+        _same_report(reps_["highs"], ref, "highs")
+        _same_report(reps_["gpu"], ref, "gpu")
+        out.append(row)
+        print(f"\n{name}: run() {t['run() total'] * 1e3:.1f} ms on the CPU path, "
+              f"{row['gpu_engine/answer_highs']['run() total'] * 1e3:.1f} ms with the GPU tables, "
+              f"{row['gpu_engine/answer_gpu']['run() total'] * 1e3:.1f} ms all on the GPU")
+    path = os.environ.get("SPX_USER_PATH_JSON")
+    if path:
+        with open(path, "w") as f:
+            json.dump({"what": "SolverController.run() stage medians (s), this build's GPU engine "
+                               "vs the oracle in place of simple_simplex (the reference's CPU "
+                               "path on this host); tests/test_gpu_user_path.py",
+                       "loadavg": list(os.getloadavg()), "cases": out}, f, indent=1)

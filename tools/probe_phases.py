@@ -34,6 +34,7 @@ def main():
     ap.add_argument("--build-only", action="store_true")
     ap.add_argument("--fmap", type=int, default=0)
     ap.add_argument("--chain", type=int, default=0, help="0 persistent chain, 1 lazy kernels")
+    ap.add_argument("--fold", type=int, default=1, help="row_fix fold (spx_set_row_fix_fold)")
     a = ap.parse_args()
     if a.build_only or not os.path.exists(LIB):
         build()
@@ -48,12 +49,15 @@ def main():
     e = DeviceTableau(0)
     e.set_window(K)
     e.set_chain(a.chain)
+    e.set_row_fix_fold(bool(a.fold))
     e.load_rows(Tf, obj, basis, a.m, 0)
     e.set_elim_variant(0, 0, -1, flush_map=a.fmap & 3)
     del Tf
     e.run_pivots(4 * K)
     e.sync()
-    e.run_pivots(K)  # one window: its stamps overwrite the buffer
+    # the last window's stamps stay in the buffer (one call: with the row_fix
+    # fold, that window rewrites the previous window's leaving rows)
+    e.run_pivots(3 * K)
     e.sync()
     lib = ctypes.CDLL(LIB)
     NB = 1024 + 2 * 8192
@@ -62,6 +66,12 @@ def main():
     t = lambda slot, kind, ph: buf[((slot * 4 + kind) * 4 + ph) & 1023]
     t0 = t(0, 0, 0)
     us = lambda x: (x - t0) / 100.0
+    if a.chain != 1 and t(K + 2, 0, 0):
+        c0 = t(K + 2, 0, 0)
+        fx = t(K + 2, 0, 1)
+        print(f"chain entry -> slot 0: {(t0 - c0) / 100.0:6.2f} us (handshake passed at "
+              f"{(t(K + 2, 0, 2) - c0) / 100.0:6.2f}" +
+              (f", fold rows stored at {(fx - c0) / 100.0:6.2f}" if fx > c0 else "") + ")")
     names = ({0: "lazy_ratio", 1: "lazy_norm"} if a.chain == 1 else
              {0: "ratio ph.", 1: "norm ph."})
     print(f"window K={K}, m={a.m}, n={a.n}: us from lazy_ratio(0) entry (block 0, thread 0)")

@@ -62,6 +62,9 @@ def main():
                     help="force a start-handshake abort of every k-th window (test hook)")
     ap.add_argument("--run-pivots", action="store_true")
     ap.add_argument("--late-drain", type=float, default=0.0)
+    ap.add_argument("--end-no-import", default="",
+                    help="after the checked LPs, reload these sizes WITHOUT a peer import "
+                         "(no pivots), check no exported buffer was freed, time the destroy")
     a = ap.parse_args()
     dist.init_process_group("gloo")
     rank, world = dist.get_rank(), dist.get_world_size()
@@ -75,6 +78,7 @@ def main():
     else:
         s = sdist.ShardedTableau(dev, rank, world, sdist.exchange_unique_id())
     runs = []
+    pool_ok = True
     import hashlib
     with s:
         s.set_window(a.window)
@@ -133,7 +137,27 @@ def main():
                 dist.gather_object(Tl, parts, dst=0)
             del Tl
             runs.append((outs, parts))
-    ok = True
+        # reloads whose buffers come back from the pool and are not
+        # exported again must return them to the pool (never hipFree), and the
+        # destroy then has no release marks to wait for in them
+        for z in [z for z in a.end_no_import.split(",") if z]:
+            rows, cols = (int(x) for x in z.split("x"))
+            r0, r1 = sdist.row_partition(rows, world, rank)
+            T, obj, basis = synth.tableau_rows(a.kind, rows, cols, a.seed, r0, r1, order="F")
+            s.load_shard(T, obj, basis, rows, r0)
+            d = s.peer_pool_debug()
+            print(f"rank {rank}: reload {rows}x{cols} without import: exported {d['exported']} "
+                  f"held {d['held']} pooled {d['pooled']}", flush=True)
+            if d["held"] != d["exported"]:
+                print(f"rank {rank}: an exported buffer was freed", flush=True)
+                pool_ok = False
+        if a.end_no_import:
+            import time
+            dist.barrier()
+            t_close = time.perf_counter()
+    if a.end_no_import:
+        print(f"rank {rank}: destroy {time.perf_counter() - t_close:.3f} s", flush=True)
+    ok = pool_ok
     if rank == 0 and not a.no_solve:
         from oracle import simplex_oracle as O
         for (rows, cols), (outs, parts) in zip(sizes, runs):
