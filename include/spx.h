@@ -54,6 +54,8 @@ extern "C" {
 #define SPX_E_RCCL (-3)
 #define SPX_E_STATE (-4)
 #define SPX_E_OOM (-5)
+#define SPX_E_NOPEER (-6) /* spx_peer_import: this load cannot run the peer chain (a rank's
+                           * exported-buffer pool is full); the RCCL path runs instead */
 
 /* pivot rules */
 #define SPX_RULE_DANTZIG 0 /* most negative reduced cost, lowest column on ties; lowest row on ratio ties */
@@ -134,8 +136,10 @@ int spx_peer_export(spx_ctx* ctx, void* out, int64_t cap);
  * context exported are never freed before spx_destroy: a
  * reload moves them to the context's pool, and later loads of that context
  * reuse the smallest pooled buffer that fits (at most 4 per buffer role; a
- * load that would need a fifth fails with SPX_E_STATE -- recreate the
- * context).  spx_destroy of an exported context waits (bounded, 10 s) for
+ * load that would need a fifth gets plain buffers that are never exported:
+ * spx_peer_import then returns SPX_E_NOPEER on every rank, the windows of
+ * that load run the RCCL path where a communicator exists, and the next load
+ * frees them -- round 5 failed the load instead).  spx_destroy of an exported context waits (bounded, 10 s) for
  * every peer to release its IPC mapping, so the ranks should destroy
  * together. */
 int spx_peer_import(spx_ctx* ctx, const void* blobs, int nranks);
@@ -213,10 +217,11 @@ int spx_pivot_at(spx_ctx* ctx, int64_t r, int64_t c);
  * together -- the rerun is again a cross-rank persistent chain.  A rank that
  * drains late is waited for: the early ranks' rerun windows abort at the
  * handshake (100 ms each) and are rerun until it arrives, which the late
- * rank catches up with at once (tested with a 0.6 s lag on one GPU).  Past
- * 16 consecutive aborts (~1.7 s) the early ranks give up with SPX_E_STATE;
- * ranks on different GPUs end in ST_FAULT after the ~4 s wait for the other
- * GPUs' verdicts.  bench.py and dist.py drain every rank right after the
+ * rank catches up with at once (tested with 0.6 s and 2.5 s lags on one
+ * GPU).  The early ranks give up with SPX_E_STATE only after rerunning for 30
+ * s (SPX_PEER_RERUN_S; round 5: after 16 aborts, ~1.7 s); ranks on different
+ * GPUs still end in ST_FAULT after the ~4 s wait for the other GPUs'
+ * verdicts (a verdict, once given, cannot be taken back consistently).  bench.py and dist.py drain every rank right after the
  * call, behind a barrier.  (2) The call's persistent-chain admission
  * (spx_set_chain_budget) is held until that drain, or until another call or
  * admission decision of this process sees the call's work complete; a

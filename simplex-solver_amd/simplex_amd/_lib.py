@@ -24,6 +24,7 @@ SPX_E_ARG = -1
 SPX_E_HIP = -2
 SPX_E_RCCL = -3
 SPX_E_STATE = -4
+SPX_E_NOPEER = -6
 
 SPX_RULE_DANTZIG = 0
 SPX_RULE_BLAND = 1

@@ -81,7 +81,7 @@ class ShardedTableau(DeviceTableau):
         super().__init__(device, _sharded=(rank, world, uid, local))
         self.rank, self.world, self.local = rank, world, local
 
-    def enable_peer_chain(self, allgather=None, push: bool | None = None) -> None:
+    def enable_peer_chain(self, allgather=None, push: bool | None = None) -> bool:
         """Set up the row-sharded persistent chain for the loaded rows (DESIGN.md
         §5): every rank calls this after its load.  Virtual ranks meet in
         process; otherwise this rank's blob (IPC handles of its tableau and
@@ -90,13 +90,16 @@ class ShardedTableau(DeviceTableau):
         push: the leaving-row transport (None: keep the context's setting;
         False pull from the owner's tableau, True owner-push into every peer's
         inbox; every rank must pass the same).  Calling it again re-imports,
-        e.g. to switch the transport between windows."""
+        e.g. to switch the transport between windows.  Returns True, or False
+        when a rank's pool of exported buffers is full for this load
+        (SPX_E_NOPEER, the same on every rank): the windows then run the RCCL
+        path -- a peer-only shard (local="peer") has none and raises."""
         lib = self._lib
         if push is not None:
             self.set_peer_push(push)
         if self.local is True:
             self._check(lib.spx_peer_chain_local(self._ctx), "spx_peer_chain_local")
-            return
+            return True
         size = lib.spx_peer_blob_size()
         buf = ctypes.create_string_buffer(size)
         self._check(lib.spx_peer_export(self._ctx, buf, size), "spx_peer_export")
@@ -110,8 +113,11 @@ class ShardedTableau(DeviceTableau):
         blobs = allgather(buf.raw)
         if len(blobs) != self.world or any(len(b) != size for b in blobs):
             raise RuntimeError("peer chain: bad blob exchange")
-        self._check(lib.spx_peer_import(self._ctx, b"".join(blobs), self.world),
-                    "spx_peer_import")
+        rc = lib.spx_peer_import(self._ctx, b"".join(blobs), self.world)
+        if rc == L.SPX_E_NOPEER and self.local is False:
+            return False
+        self._check(rc, "spx_peer_import")
+        return True
 
     def set_peer_push(self, on: bool) -> None:
         """Leaving-row transport for the next enable_peer_chain (spx_set_peer_push)."""

@@ -11,7 +11,10 @@ the "z_j - c_j" form of a MAX problem, right-hand side in the last column;
 """
 from __future__ import annotations
 
+import atexit
 import ctypes
+import os
+import threading
 from dataclasses import dataclass
 
 import numpy as np
@@ -401,3 +404,67 @@ class DeviceTableau:
         self._check(self._lib.spx_set_elim_variant(self._ctx, int(R), int(target_wgs),
                                                    int(nt_flags), int(interleave)),
                     "spx_set_elim_variant")
+
+
+class ContextPool:
+    """Idle single-GPU contexts, reused by the solves of small LPs.
+
+    The reference's user path (/solve, app/controllers/solver_controller.py:
+    53-120, 290-319) solves textbook-sized LPs, where creating and destroying
+    an spx context (a HIP stream, events, pinned host State, device buffers:
+    ~2 ms each way, tests/test_gpu_user_path.py) costs more than the pivots.
+    ``lp.solve_standard_form`` therefore takes a context from this pool and
+    gives it back: at most `cap` idle contexts per device (SPX_CONTEXT_POOL,
+    default 8; 0 disables), only for tableaux of at most `max_cells` cells (a
+    pooled context keeps its last tableau in HBM), never one whose solve
+    raised.  Thread-safe (the reference's /solve runs from many threads,
+    tests/test_performance_load.py:80-83); a forked child never reuses its
+    parent's contexts (a HIP context does not survive fork)."""
+
+    def __init__(self, cap: int | None = None, max_cells: int = 1 << 22):
+        self.cap = int(os.environ.get("SPX_CONTEXT_POOL", "8")) if cap is None else cap
+        self.max_cells = max_cells
+        self._lock = threading.Lock()
+        self._idle: dict = {}
+        self._pid = os.getpid()
+
+    def _fresh(self) -> None:
+        if self._pid != os.getpid():  # (held by the lock's owner)
+            self._idle = {}
+            self._pid = os.getpid()
+
+    def acquire(self, device: int = 0) -> "DeviceTableau":
+        with self._lock:
+            self._fresh()
+            free = self._idle.get(device)
+            eng = free.pop() if free else None
+        if eng is None:
+            return DeviceTableau(device)
+        eng.set_window(0)  # (the knob lp.py's solves change; the load resets the rest)
+        return eng
+
+    def release(self, eng: "DeviceTableau", reusable: bool = True) -> None:
+        keep = (reusable and self.cap > 0 and not eng.sharded and getattr(eng, "_ctx", None)
+                and (eng.m_local + 1) * eng.N <= self.max_cells)
+        if keep:
+            with self._lock:
+                self._fresh()
+                free = self._idle.setdefault(eng.device, [])
+                if len(free) < self.cap:
+                    free.append(eng)
+                    return
+        eng.close()
+
+    def clear(self) -> None:
+        with self._lock:
+            idle, self._idle = self._idle, {}
+            mine = self._pid == os.getpid()
+        if mine:
+            for free in idle.values():
+                for eng in free:
+                    eng.close()
+
+
+POOL = ContextPool()
+atexit.register(POOL.clear)
+

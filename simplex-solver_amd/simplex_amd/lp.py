@@ -31,7 +31,7 @@ from typing import Callable, List, Optional, Sequence
 
 import numpy as np
 
-from .engine import DeviceTableau, SolveResult, auto_window
+from .engine import POOL, DeviceTableau, SolveResult, auto_window
 from . import _lib as L
 
 OPS = {"<=": "L", "L": "L", ">=": "G", "G": "G", "=": "E", "==": "E", "E": "E"}
@@ -221,7 +221,9 @@ def solve_standard_form(sf: StandardForm, *, device: int = 0, rule: str = "dantz
     """Two-phase tableau simplex of a StandardForm on the GPU engine.
     window: pivots per tableau pass for the unrecorded stretch of each phase
     (-1: auto_window by size; 0: one pass per pivot)."""
-    eng = engine_factory() if engine_factory else DeviceTableau(device)
+    # (a pooled context unless the caller brings its own: engine.ContextPool)
+    eng = engine_factory() if engine_factory else POOL.acquire(device)
+    reusable = True  # (a context whose solve raised is destroyed, never pooled)
     if window < 0:
         window = auto_window(sf.m, sf.N)
     try:
@@ -269,8 +271,14 @@ def solve_standard_form(sf: StandardForm, *, device: int = 0, rule: str = "dantz
         zmax = eng.objective_row()[-1]
         z = float(zmax if sf.maximize else -zmax)
         return LPResult(L.SPX_OPTIMAL, x, z, iters, basis, pivots, rec.steps)
+    except BaseException:
+        reusable = False
+        raise
     finally:
-        eng.close()
+        if engine_factory:
+            eng.close()
+        else:
+            POOL.release(eng, reusable)
 
 
 def solve_lp(c, rows, maximize=True, **kw) -> LPResult:
