@@ -661,6 +661,224 @@ __device__ __forceinline__ double sys_load(const double* p) {
       (gu64*)const_cast<double*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
 }
 
+// The pending slots 0..q-1 of a window applied to one stale value, as masks
+// ("Slot application as masks"; LEAN: slots >= q are exact
+// identities on +0 histories), shared by chain_kernel and chain_shard_kernel
+// (one implementation of each phase's slot chain; forceinline, so each kernel
+// compiles the same code as when the loops were written out in it).
+// ratio_slots: column c on my row `row` (its f history fs, lane s of pcl =
+// p_s[c]; rmask: slots my row left at).
+template <int KMAX, int CH, bool LEAN>
+__device__ __forceinline__ double ratio_slots(double fv, const double (&fs)[KMAX], double pcl,
+                                              uint32_t rmask, int q, int64_t row, int64_t c,
+                                              int64_t slot_r, int64_t slot_c, bool skip) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t qm = (1u << q) - 1u;
+  if (__ballot(lane < q && (slot_c == c || (skip && pcl == 0.0))) == 0ull) {
+    if (__ballot((rmask & qm) != 0u) == 0ull) {
+#pragma unroll
+      for (int c8 = 0; c8 < KMAX; c8 += CH) {
+        if (c8 < q) {
+#pragma unroll
+          for (int u = 0; u < CH; ++u) {
+            const int s = c8 + u;
+            const double x = msub(fv, fs[s], rdlane(pcl, s));
+            if constexpr (LEAN) fv = x;  // (s >= q: +0 histories, an identity)
+            else fv = s < q ? x : fv;
+          }
+        }
+      }
+    } else {
+#pragma unroll
+      for (int c8 = 0; c8 < KMAX; c8 += CH) {
+        if (c8 < q) {
+#pragma unroll
+          for (int u = 0; u < CH; ++u) {
+            const int s = c8 + u;
+            const double p_s = rdlane(pcl, s);
+            double x = msub(fv, fs[s], p_s);
+            x = ((rmask >> s) & 1u) ? p_s : x;  // (bit s >= q is never set)
+            if constexpr (LEAN) fv = x;
+            else fv = s < q ? x : fv;
+          }
+        }
+      }
+    }
+  } else {
+#pragma unroll
+    for (int c8 = 0; c8 < KMAX; c8 += CH) {
+      if (c8 < q) {
+#pragma unroll
+        for (int u = 0; u < CH; ++u) {
+          const int s = c8 + u;
+          const bool act = s < q;
+          const bool isr = row == rdlane64(slot_r, s);
+          const bool isc = c == rdlane64(slot_c, s);
+          fv = apply_sel(fv, isr, isc, act, fs[s], rdlane(pcl, s), skip);
+        }
+      }
+    }
+  }
+  return fv;
+}
+// norm_slots: row r on my column jc (its p history ps, lane s of frl = f_s[r],
+// lane q the pivot element; zmask / cmask: slots whose p_s[jc] was 0 under the
+// skip rule / that entered jc).
+template <int KMAX, int CH, bool LEAN>
+__device__ __forceinline__ double norm_slots(double v, const double (&ps)[KMAX], double frl,
+                                             uint32_t zmask, uint32_t cmask, int q, bool jlive,
+                                             int64_t r, int64_t jc, int64_t slot_r,
+                                             int64_t slot_c, bool skip) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t qmn = (1u << q) - 1u;
+  const double frm = LEAN ? (lane < q ? frl : 0.0) : frl;
+  if (__ballot(lane < q && slot_r == r) == 0ull) {
+    if (__ballot(jlive && ((zmask | cmask) & qmn) != 0u) == 0ull) {
+#pragma unroll
+      for (int c8 = 0; c8 < KMAX; c8 += CH) {
+        if (c8 < q) {
+#pragma unroll
+          for (int u = 0; u < CH; ++u) {
+            const int s = c8 + u;
+            const double x = msub(v, rdlane(frm, s), ps[s]);
+            if constexpr (LEAN) v = x;  // (s >= q: +0 histories, an identity)
+            else v = s < q ? x : v;
+          }
+        }
+      }
+    } else {
+#pragma unroll
+      for (int c8 = 0; c8 < KMAX; c8 += CH) {
+        if (c8 < q) {
+#pragma unroll
+          for (int u = 0; u < CH; ++u) {
+            const int s = c8 + u;
+            double x = msub(v, rdlane(frm, s), ps[s]);
+            x = ((zmask >> s) & 1u) ? v : x;  // (bits s >= q are never set)
+            x = ((cmask >> s) & 1u) ? 0.0 : x;
+            if constexpr (LEAN) v = x;
+            else v = s < q ? x : v;
+          }
+        }
+      }
+    }
+  } else {
+#pragma unroll
+    for (int c8 = 0; c8 < KMAX; c8 += CH) {
+      if (c8 < q) {
+#pragma unroll
+        for (int u = 0; u < CH; ++u) {
+          const int s = c8 + u;
+          const bool act = s < q;
+          const bool isr = r == rdlane64(slot_r, s);
+          const bool isc = jc == rdlane64(slot_c, s);
+          v = apply_sel(v, isr, isc, act, rdlane(frl, s), ps[s], skip);
+        }
+      }
+    }
+  }
+  return v;
+}
+
+// The norm phase's update of my column at slot q (lazy_norm's arithmetic):
+// p_q = v / piv, the skip / entered masks, the objective entry, the column
+// tag and the entering key for pivot q+1; the RHS column (xown) the same with
+// p = prhs (p_q[rhs]).  Shared by both chain kernels (forceinline).
+template <int KMAX, bool LH>
+__device__ __forceinline__ void norm_update(KeyP& ek, double& pq, double (&ps)[KMAX],
+                                            uint32_t& zmask, uint32_t& cmask, double& o,
+                                            uint32_t& tg, bool jlive, int64_t j, int64_t c, int q,
+                                            double v, double piv, double zc, bool skip, bool zb,
+                                            uint32_t W, int64_t n_enter, double eps_opt,
+                                            int32_t rule, bool xown, uint32_t& zmx, double& ox,
+                                            uint32_t& tgx, double prhs, uint32_t qmn,
+                                            double* pxl) {
+  ek = keyp_none();
+  pq = 0.0;
+  if (jlive) {
+    const double p = v / piv;
+    pq = p;
+    zmask |= (skip && p == 0.0) ? (1u << q) : 0u;
+    cmask |= (j == c) ? (1u << q) : 0u;
+    if constexpr (!LH) {
+#pragma unroll
+      for (int s = 0; s < KMAX; ++s) ps[s] = (s == q) ? p : ps[s];
+    }
+    const bool nz = (p != 0.0) || !skip;
+    if (j == c) {
+      o = 0.0;
+    } else if (nz) {
+      o = msub(o, zc, p);
+    }
+    const bool tagged = (tg & TAG_EPOCH) == W;
+    if (nz) {
+      tg = W | ((j == c || (tagged && (tg & TAG_SPECIAL))) ? TAG_SPECIAL : 0u) |
+           (zb ? TAG_ZERO : 0u);
+    } else if (tagged) {
+      tg = tg | TAG_ZERO;
+    }
+    // key (o, j) under Dantzig, (0, j) under Bland; payload o (z_c)
+    if (j < n_enter && o < -eps_opt) kmin2(ek, rule == RULE_BLAND ? 0.0 : o, j, j, o, 0.0);
+  }
+  if (xown) {  // the RHS column: the same update with p = p_q[rhs] (never j == c)
+    const bool zbx = (zmx & qmn) != 0u;
+    zmx |= (skip && prhs == 0.0) ? (1u << q) : 0u;
+    const bool nz = (prhs != 0.0) || !skip;
+    if (nz) ox = msub(ox, zc, prhs);
+    const bool tagged = (tgx & TAG_EPOCH) == W;
+    if (nz) {
+      tgx = W | ((tagged && (tgx & TAG_SPECIAL)) ? TAG_SPECIAL : 0u) | (zbx ? TAG_ZERO : 0u);
+    } else if (tagged) {
+      tgx = tgx | TAG_ZERO;
+    }
+    pxl[q] = prhs;
+  }
+}
+
+// The window's touched columns compacted into the flush's records (as
+// lazy_norm's last slot): wave ballot + LDS prefix + one atomic per block;
+// the RHS column (xown) follows its wave's own columns.  pget(s) = my column's
+// p_s.  Shared by both chain kernels (forceinline).
+template <int KMAX, int NW, typename PGet>
+__device__ __forceinline__ void compact_records(const Window& win, int64_t N, int q, uint32_t W,
+                                                bool jlive, bool xown, int64_t j, uint32_t tg,
+                                                uint32_t tgx, const double* pxl, int t, int lane,
+                                                int w, int* wcnt, int& base, PGet pget) {
+  const bool mine = jlive && (tg & TAG_EPOCH) == W;
+  const bool minex = xown && (tgx & TAG_EPOCH) == W;
+  const uint64_t bal = __ballot(mine);
+  const uint64_t balx = __ballot(minex);
+  if (lane == 0) wcnt[w] = __popcll(bal) + __popcll(balx);
+  __syncthreads();
+  if (t == 0) {
+    int tot = 0;
+    for (int x = 0; x < NW; ++x) tot += wcnt[x];
+    base = tot ? (int)__hip_atomic_fetch_add((gu32*)win.nlist, (unsigned)tot, __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT)
+               : 0;
+  }
+  __syncthreads();
+  int pos = base + __popcll(bal & ((1ull << lane) - 1ull));
+  for (int x = 0; x < w; ++x) pos += wcnt[x];
+  if (mine && pos < N) {
+    double* rc_ = win.rec + (int64_t)pos * RECW;
+    reinterpret_cast<int64_t*>(rc_)[0] = j | ((int64_t)(tg >> 30) << 32);
+#pragma unroll
+    for (int s = 0; s < KMAX; ++s)
+      if (s < q) rc_[2 + s] = pget(s);
+  }
+  if (minex) {
+    const int px = pos - __popcll(bal & ((1ull << lane) - 1ull)) + __popcll(bal);
+    if (px < N) {
+      double* rc_ = win.rec + (int64_t)px * RECW;
+      reinterpret_cast<int64_t*>(rc_)[0] = (N - 1) | ((int64_t)(tgx >> 30) << 32);
+#pragma unroll
+      for (int s = 0; s < KMAX; ++s)
+        if (s < q) rc_[2 + s] = pxl[s];
+    }
+  }
+}
+
 // ---------------------------------------------------------------------------
 // chain_kernel<KMAX, CB>: the pivots of one window (npiv <= KMAX slots) on one
 // GPU.  grid = B blocks of CB threads (one block per CU, every block
@@ -984,52 +1202,7 @@ __global__ __launch_bounds__(CB) void chain_kernel(
     // window or p_s[c] == 0 under the skip rule (uniform: the exact loop), my
     // row left at slot s (rmask: p_s[c] replaces the msub on that lane).
     // Otherwise a slot is one msub (~5 VALU ops instead of ~25).
-    const uint32_t qm = (1u << q) - 1u;
-    if (__ballot(lane < q && (slot_c == c || (skip && pcl == 0.0))) == 0ull) {
-      if (__ballot((rmask & qm) != 0u) == 0ull) {
-#pragma unroll
-        for (int c8 = 0; c8 < KMAX; c8 += CH) {
-          if (c8 < q) {
-#pragma unroll
-            for (int u = 0; u < CH; ++u) {
-              const int s = c8 + u;
-              const double x = msub(fv, fs[s], rdlane(pcl, s));
-              if constexpr (LEAN) fv = x;  // (s >= q: +0 histories, an identity)
-              else fv = s < q ? x : fv;
-            }
-          }
-        }
-      } else {
-#pragma unroll
-        for (int c8 = 0; c8 < KMAX; c8 += CH) {
-          if (c8 < q) {
-#pragma unroll
-            for (int u = 0; u < CH; ++u) {
-              const int s = c8 + u;
-              const double p_s = rdlane(pcl, s);
-              double x = msub(fv, fs[s], p_s);
-              x = ((rmask >> s) & 1u) ? p_s : x;  // (bit s >= q is never set)
-              if constexpr (LEAN) fv = x;
-              else fv = s < q ? x : fv;
-            }
-          }
-        }
-      }
-    } else {
-#pragma unroll
-      for (int c8 = 0; c8 < KMAX; c8 += CH) {
-        if (c8 < q) {
-#pragma unroll
-          for (int u = 0; u < CH; ++u) {
-            const int s = c8 + u;
-            const bool act = s < q;
-            const bool isr = i == rdlane64(slot_r, s);
-            const bool isc = c == rdlane64(slot_c, s);
-            fv = apply_sel(fv, isr, isc, act, fs[s], rdlane(pcl, s), skip);
-          }
-        }
-      }
-    }
+    fv = ratio_slots<KMAX, CH, LEAN>(fv, fs, pcl, rmask, q, i, c, slot_r, slot_c, skip);
     SPX_PROBE(q, 2, 1, fv != 12345.678);  // slots applied
     SPX_PROBE_CHAIN_T(q, 6, fv != 12345.678);
     if constexpr (LH) {
@@ -1132,94 +1305,13 @@ __global__ __launch_bounds__(CB) void chain_kernel(
     const bool zb = (zmask & qmn) != 0u;
     // LEAN: lane q holds the pivot element, which slot q of a chunk must not
     // see (piv * +0 may be -0); lanes > q are +0 already
-    const double frm = LEAN ? (lane < q ? frl : 0.0) : frl;
-    if (__ballot(lane < q && slot_r == r) == 0ull) {
-      if (__ballot(jlive && ((zmask | cmask) & qmn) != 0u) == 0ull) {
-#pragma unroll
-        for (int c8 = 0; c8 < KMAX; c8 += CH) {
-          if (c8 < q) {
-#pragma unroll
-            for (int u = 0; u < CH; ++u) {
-              const int s = c8 + u;
-              const double x = msub(v, rdlane(frm, s), ps[s]);
-              if constexpr (LEAN) v = x;  // (s >= q: +0 histories, an identity)
-              else v = s < q ? x : v;
-            }
-          }
-        }
-      } else {
-#pragma unroll
-        for (int c8 = 0; c8 < KMAX; c8 += CH) {
-          if (c8 < q) {
-#pragma unroll
-            for (int u = 0; u < CH; ++u) {
-              const int s = c8 + u;
-              double x = msub(v, rdlane(frm, s), ps[s]);
-              x = ((zmask >> s) & 1u) ? v : x;  // (bits s >= q are never set)
-              x = ((cmask >> s) & 1u) ? 0.0 : x;
-              if constexpr (LEAN) v = x;
-              else v = s < q ? x : v;
-            }
-          }
-        }
-      }
-    } else {
-#pragma unroll
-      for (int c8 = 0; c8 < KMAX; c8 += CH) {
-        if (c8 < q) {
-#pragma unroll
-          for (int u = 0; u < CH; ++u) {
-            const int s = c8 + u;
-            const bool act = s < q;
-            const bool isr = r == rdlane64(slot_r, s);
-            const bool isc = jc == rdlane64(slot_c, s);
-            v = apply_sel(v, isr, isc, act, rdlane(frl, s), ps[s], skip);
-          }
-        }
-      }
-    }
+    v = norm_slots<KMAX, CH, LEAN>(v, ps, frl, zmask, cmask, q, jlive, r, jc, slot_r, slot_c, skip);
     SPX_PROBE(q, 3, 1, v != 12345.678);  // slots applied
     SPX_PROBE_CHAIN_T(q, 7, v != 12345.678);
-    KeyP ek = keyp_none();
-    double pq = 0.0;  // p_q[j]
-    if (jlive) {
-      const double p = v / piv;
-      pq = p;
-      zmask |= (skip && p == 0.0) ? (1u << q) : 0u;
-      cmask |= (j == c) ? (1u << q) : 0u;
-      if constexpr (!LH) {
-#pragma unroll
-        for (int s = 0; s < KMAX; ++s) ps[s] = (s == q) ? p : ps[s];
-      }
-      const bool nz = (p != 0.0) || !skip;
-      if (j == c) {
-        o = 0.0;
-      } else if (nz) {
-        o = msub(o, zc, p);
-      }
-      const bool tagged = (tg & TAG_EPOCH) == W;
-      if (nz) {
-        tg = W | ((j == c || (tagged && (tg & TAG_SPECIAL))) ? TAG_SPECIAL : 0u) |
-             (zb ? TAG_ZERO : 0u);
-      } else if (tagged) {
-        tg = tg | TAG_ZERO;
-      }
-      // key (o, j) under Dantzig, (0, j) under Bland; payload o (z_c)
-      if (j < n_enter && o < -eps_opt) kmin2(ek, rule == RULE_BLAND ? 0.0 : o, j, j, o, 0.0);
-    }
-    if (xown) {  // the RHS column: the same update with p = p_q[rhs] (never j == c)
-      const bool zbx = (zmx & qmn) != 0u;
-      zmx |= (skip && prhs == 0.0) ? (1u << q) : 0u;
-      const bool nz = (prhs != 0.0) || !skip;
-      if (nz) ox = msub(ox, zc, prhs);
-      const bool tagged = (tgx & TAG_EPOCH) == W;
-      if (nz) {
-        tgx = W | ((tagged && (tgx & TAG_SPECIAL)) ? TAG_SPECIAL : 0u) | (zbx ? TAG_ZERO : 0u);
-      } else if (tagged) {
-        tgx = tgx | TAG_ZERO;
-      }
-      pxl[q] = prhs;
-    }
+    KeyP ek;
+    double pq;  // p_q[j]
+    norm_update<KMAX, LH>(ek, pq, ps, zmask, cmask, o, tg, jlive, j, c, q, v, piv, zc, skip, zb, W,
+                          n_enter, eps_opt, rule, xown, zmx, ox, tgx, prhs, qmn, pxl);
     if (ilive && i == r) bas = c;
     rmask |= (i == r) ? (1u << q) : 0u;
     if (lane == q) {
@@ -1319,41 +1411,13 @@ __global__ __launch_bounds__(CB) void chain_kernel(
   // compact the window's touched columns into records for the flush (as
   // lazy_norm's last slot): wave ballot + LDS prefix + one atomic per block;
   // the RHS column (xown) follows its wave's own columns
-  const bool mine = jlive && (tg & TAG_EPOCH) == W;
-  const bool minex = xown && (tgx & TAG_EPOCH) == W;
   __shared__ int wcnt[NW];
   __shared__ int base;
-  const uint64_t bal = __ballot(mine);
-  const uint64_t balx = __ballot(minex);
-  if (lane == 0) wcnt[w] = __popcll(bal) + __popcll(balx);
-  __syncthreads();
-  if (t == 0) {
-    int tot = 0;
-    for (int x = 0; x < NW; ++x) tot += wcnt[x];
-    base = tot ? (int)__hip_atomic_fetch_add((gu32*)win.nlist, (unsigned)tot, __ATOMIC_RELAXED,
-                                             __HIP_MEMORY_SCOPE_AGENT)
-               : 0;
-  }
-  __syncthreads();
-  int pos = base + __popcll(bal & ((1ull << lane) - 1ull));
-  for (int x = 0; x < w; ++x) pos += wcnt[x];
-  if (mine && pos < N) {
-    double* rc_ = win.rec + (int64_t)pos * RECW;
-    reinterpret_cast<int64_t*>(rc_)[0] = j | ((int64_t)(tg >> 30) << 32);
-#pragma unroll
-    for (int s = 0; s < KMAX; ++s)
-      if (s < q) rc_[2 + s] = LH ? psl[s][t] : ps[s];
-  }
-  if (minex) {
-    const int px = pos - __popcll(bal & ((1ull << lane) - 1ull)) + __popcll(bal);
-    if (px < N) {
-      double* rc_ = win.rec + (int64_t)px * RECW;
-      reinterpret_cast<int64_t*>(rc_)[0] = (N - 1) | ((int64_t)(tgx >> 30) << 32);
-#pragma unroll
-      for (int s = 0; s < KMAX; ++s)
-        if (s < q) rc_[2 + s] = pxl[s];
-    }
-  }
+  compact_records<KMAX, NW>(win, N, q, W, jlive, xown, j, tg, tgx, pxl, t, lane, w, wcnt, base,
+                            [&](int s) -> double {
+                              if constexpr (LH) return psl[s][t];
+                              else return ps[s];
+                            });
 }
 
 // ---------------------------------------------------------------------------
@@ -1593,52 +1657,7 @@ __global__ __launch_bounds__(CB) void chain_shard_kernel(
     // window or p_s[c] == 0 under the skip rule (uniform: the exact loop), my
     // row left at slot s (rmask: p_s[c] replaces the msub on that lane).
     // Otherwise a slot is one msub (~5 VALU ops instead of ~25).
-    const uint32_t qm = (1u << q) - 1u;
-    if (__ballot(lane < q && (slot_c == c || (skip && pcl == 0.0))) == 0ull) {
-      if (__ballot((rmask & qm) != 0u) == 0ull) {
-#pragma unroll
-        for (int c8 = 0; c8 < KMAX; c8 += CH) {
-          if (c8 < q) {
-#pragma unroll
-            for (int u = 0; u < CH; ++u) {
-              const int s = c8 + u;
-              const double x = msub(fv, fs[s], rdlane(pcl, s));
-              if constexpr (LEAN) fv = x;  // (s >= q: +0 histories, an identity)
-              else fv = s < q ? x : fv;
-            }
-          }
-        }
-      } else {
-#pragma unroll
-        for (int c8 = 0; c8 < KMAX; c8 += CH) {
-          if (c8 < q) {
-#pragma unroll
-            for (int u = 0; u < CH; ++u) {
-              const int s = c8 + u;
-              const double p_s = rdlane(pcl, s);
-              double x = msub(fv, fs[s], p_s);
-              x = ((rmask >> s) & 1u) ? p_s : x;  // (bit s >= q is never set)
-              if constexpr (LEAN) fv = x;
-              else fv = s < q ? x : fv;
-            }
-          }
-        }
-      }
-    } else {
-#pragma unroll
-      for (int c8 = 0; c8 < KMAX; c8 += CH) {
-        if (c8 < q) {
-#pragma unroll
-          for (int u = 0; u < CH; ++u) {
-            const int s = c8 + u;
-            const bool act = s < q;
-            const bool isr = ig == rdlane64(slot_r, s);
-            const bool isc = c == rdlane64(slot_c, s);
-            fv = apply_sel(fv, isr, isc, act, fs[s], rdlane(pcl, s), skip);
-          }
-        }
-      }
-    }
+    fv = ratio_slots<KMAX, CH, LEAN>(fv, fs, pcl, rmask, q, ig, c, slot_r, slot_c, skip);
     SPX_PROBE(q, 2, 1, fv != 12345.678);  // slots applied
     if constexpr (LH) {
       fsl[q][t] = fv;
@@ -1772,93 +1791,12 @@ __global__ __launch_bounds__(CB) void chain_shard_kernel(
     const bool zb = (zmask & qmn) != 0u;
     // LEAN: lane q holds the pivot element, which slot q of a chunk must not
     // see (piv * +0 may be -0); lanes > q are +0 already
-    const double frm = LEAN ? (lane < q ? frl : 0.0) : frl;
-    if (__ballot(lane < q && slot_r == r) == 0ull) {
-      if (__ballot(jlive && ((zmask | cmask) & qmn) != 0u) == 0ull) {
-#pragma unroll
-        for (int c8 = 0; c8 < KMAX; c8 += CH) {
-          if (c8 < q) {
-#pragma unroll
-            for (int u = 0; u < CH; ++u) {
-              const int s = c8 + u;
-              const double x = msub(v, rdlane(frm, s), ps[s]);
-              if constexpr (LEAN) v = x;  // (s >= q: +0 histories, an identity)
-              else v = s < q ? x : v;
-            }
-          }
-        }
-      } else {
-#pragma unroll
-        for (int c8 = 0; c8 < KMAX; c8 += CH) {
-          if (c8 < q) {
-#pragma unroll
-            for (int u = 0; u < CH; ++u) {
-              const int s = c8 + u;
-              double x = msub(v, rdlane(frm, s), ps[s]);
-              x = ((zmask >> s) & 1u) ? v : x;  // (bits s >= q are never set)
-              x = ((cmask >> s) & 1u) ? 0.0 : x;
-              if constexpr (LEAN) v = x;
-              else v = s < q ? x : v;
-            }
-          }
-        }
-      }
-    } else {
-#pragma unroll
-      for (int c8 = 0; c8 < KMAX; c8 += CH) {
-        if (c8 < q) {
-#pragma unroll
-          for (int u = 0; u < CH; ++u) {
-            const int s = c8 + u;
-            const bool act = s < q;
-            const bool isr = r == rdlane64(slot_r, s);
-            const bool isc = jc == rdlane64(slot_c, s);
-            v = apply_sel(v, isr, isc, act, rdlane(frl, s), ps[s], skip);
-          }
-        }
-      }
-    }
+    v = norm_slots<KMAX, CH, LEAN>(v, ps, frl, zmask, cmask, q, jlive, r, jc, slot_r, slot_c, skip);
     SPX_PROBE(q, 3, 1, v != 12345.678);  // slots applied
-    KeyP ek = keyp_none();
-    double pq = 0.0;  // p_q[j]
-    if (jlive) {
-      const double p = v / piv;
-      pq = p;
-      zmask |= (skip && p == 0.0) ? (1u << q) : 0u;
-      cmask |= (j == c) ? (1u << q) : 0u;
-      if constexpr (!LH) {
-#pragma unroll
-        for (int s = 0; s < KMAX; ++s) ps[s] = (s == q) ? p : ps[s];
-      }
-      const bool nz = (p != 0.0) || !skip;
-      if (j == c) {
-        o = 0.0;
-      } else if (nz) {
-        o = msub(o, zc, p);
-      }
-      const bool tagged = (tg & TAG_EPOCH) == W;
-      if (nz) {
-        tg = W | ((j == c || (tagged && (tg & TAG_SPECIAL))) ? TAG_SPECIAL : 0u) |
-             (zb ? TAG_ZERO : 0u);
-      } else if (tagged) {
-        tg = tg | TAG_ZERO;
-      }
-      // key (o, j) under Dantzig, (0, j) under Bland; payload o (z_c)
-      if (j < n_enter && o < -eps_opt) kmin2(ek, rule == RULE_BLAND ? 0.0 : o, j, j, o, 0.0);
-    }
-    if (xown) {  // the RHS column: the same update with p = p_q[rhs] (never j == c)
-      const bool zbx = (zmx & qmn) != 0u;
-      zmx |= (skip && prhs == 0.0) ? (1u << q) : 0u;
-      const bool nz = (prhs != 0.0) || !skip;
-      if (nz) ox = msub(ox, zc, prhs);
-      const bool tagged = (tgx & TAG_EPOCH) == W;
-      if (nz) {
-        tgx = W | ((tagged && (tgx & TAG_SPECIAL)) ? TAG_SPECIAL : 0u) | (zbx ? TAG_ZERO : 0u);
-      } else if (tagged) {
-        tgx = tgx | TAG_ZERO;
-      }
-      pxl[q] = prhs;
-    }
+    KeyP ek;
+    double pq;  // p_q[j]
+    norm_update<KMAX, LH>(ek, pq, ps, zmask, cmask, o, tg, jlive, j, c, q, v, piv, zc, skip, zb, W,
+                          n_enter, eps_opt, rule, xown, zmx, ox, tgx, prhs, qmn, pxl);
     if (ilive && ig == r) bas = c;
     rmask |= (ig == r) ? (1u << q) : 0u;
     if (lane == q) {
@@ -1961,41 +1899,13 @@ __global__ __launch_bounds__(CB) void chain_shard_kernel(
   // compact the window's touched columns into records for the flush (as
   // lazy_norm's last slot): wave ballot + LDS prefix + one atomic per block;
   // the RHS column (xown) follows its wave's own columns
-  const bool mine = jlive && (tg & TAG_EPOCH) == W;
-  const bool minex = xown && (tgx & TAG_EPOCH) == W;
   __shared__ int wcnt[NW];
   __shared__ int base;
-  const uint64_t bal = __ballot(mine);
-  const uint64_t balx = __ballot(minex);
-  if (lane == 0) wcnt[w] = __popcll(bal) + __popcll(balx);
-  __syncthreads();
-  if (t == 0) {
-    int tot = 0;
-    for (int x = 0; x < NW; ++x) tot += wcnt[x];
-    base = tot ? (int)__hip_atomic_fetch_add((gu32*)win.nlist, (unsigned)tot, __ATOMIC_RELAXED,
-                                             __HIP_MEMORY_SCOPE_AGENT)
-               : 0;
-  }
-  __syncthreads();
-  int pos = base + __popcll(bal & ((1ull << lane) - 1ull));
-  for (int x = 0; x < w; ++x) pos += wcnt[x];
-  if (mine && pos < N) {
-    double* rc_ = win.rec + (int64_t)pos * RECW;
-    reinterpret_cast<int64_t*>(rc_)[0] = j | ((int64_t)(tg >> 30) << 32);
-#pragma unroll
-    for (int s = 0; s < KMAX; ++s)
-      if (s < q) rc_[2 + s] = LH ? psl[s][t] : ps[s];
-  }
-  if (minex) {
-    const int px = pos - __popcll(bal & ((1ull << lane) - 1ull)) + __popcll(bal);
-    if (px < N) {
-      double* rc_ = win.rec + (int64_t)px * RECW;
-      reinterpret_cast<int64_t*>(rc_)[0] = (N - 1) | ((int64_t)(tgx >> 30) << 32);
-#pragma unroll
-      for (int s = 0; s < KMAX; ++s)
-        if (s < q) rc_[2 + s] = pxl[s];
-    }
-  }
+  compact_records<KMAX, NW>(win, N, q, W, jlive, xown, j, tg, tgx, pxl, t, lane, w, wcnt, base,
+                            [&](int s) -> double {
+                              if constexpr (LH) return psl[s][t];
+                              else return ps[s];
+                            });
 }
 
 }  // namespace spx
