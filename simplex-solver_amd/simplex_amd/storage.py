@@ -238,6 +238,27 @@ def _scalar(x) -> bool:
     return x is None or isinstance(x, (bool, int, float, str))
 
 
+_enc_str = json.encoder.encode_basestring  # (the C encoder where CPython has it)
+
+
+def _scalar_dict_body(o: dict, level: int) -> Optional[str]:
+    """The lines of a dict whose values are all non-string scalars, exactly as
+    the generic branch of ``_dump`` writes them, built with C-level loops: the
+    keys through the string encoder, the values through ONE ``json.dumps`` of
+    the value list split on its ", " separators (a number, true / false / null
+    never contains one).  A constraint's coefficient dict of config 2 has
+    2,048 entries and a report holds 1,024 of them: one write per entry was
+    ~5 s of save_solution (profiles/r06/user_path.json).  None: not such a
+    dict (the generic branch runs)."""
+    vals = list(o.values())
+    if not all(_scalar(v) and not isinstance(v, str) for v in vals):
+        return None
+    enc = json.dumps(vals, ensure_ascii=False, allow_nan=True)[1:-1].split(", ")
+    ind = _IND * (level + 1)
+    keys = [ind + _enc_str(str(k)) + ": " for k in o]
+    return ",\n".join(map(str.__add__, keys, enc))
+
+
 def _dump(o: Any, f, level: int) -> None:
     """``json.dump(o, indent=4, ensure_ascii=False)`` except that a list of
     scalars (a table row, a pivot pair) goes on one line, streamed piecewise."""
@@ -245,6 +266,10 @@ def _dump(o: Any, f, level: int) -> None:
     if isinstance(o, dict):
         if not o:
             f.write("{}")
+            return
+        body = _scalar_dict_body(o, level) if len(o) > 8 else None
+        if body is not None:
+            f.write("{\n" + body + "\n" + _IND * level + "}")
             return
         f.write("{\n")
         n = len(o)

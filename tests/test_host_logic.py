@@ -232,6 +232,40 @@ def test_storage_roundtrip_and_latest(tmp_path, monkeypatch):
     assert S.get_new_pdf_path().endswith("reporte_solucion_2.pdf")
 
 
+def test_storage_scalar_dict_fast_path_same_bytes(monkeypatch):
+    """The scalar-dict fast path of the report writer (a constraint's
+    coefficient dict) gives the bytes the per-entry path gives, and both equal
+    json.dumps(indent=4) for such a dict."""
+    import io
+    import json
+    from simplex_amd import storage
+    rng = np.random.default_rng(7)
+    coef = {f"x{j:04d}": float(v) for j, v in enumerate(rng.standard_normal(300))}
+    coef.update({"nan": float("nan"), "inf": float("inf"), "-inf": float("-inf"),
+                 "negzero": -0.0, "int": 7, "big": 10 ** 30, "t": True, "f": False,
+                 "none": None, 'q"uo\\te': 1.5, "línea\n\tñ": 2.0, "f64": np.float64(0.1)})
+    doc = {"problema_definicion": {"funcion_objetivo": {"type": "maximize",
+                                                        "coefficients": coef},
+                                   "restricciones": [{"coefficients": coef, "operator": "<=",
+                                                      "rhs": 4.0}] * 3},
+           "valores": {f"x{j}": j * 0.5 for j in range(12)},
+           "mixed": {f"k{j}": ("s" if j == 5 else j) for j in range(12)},
+           "small": {"a": 1.0}}
+
+    def dump():
+        buf = io.StringIO()
+        storage._dump(doc, buf, 0)
+        return buf.getvalue()
+
+    fast = dump()
+    monkeypatch.setattr(storage, "_scalar_dict_body", lambda o, level: None)
+    assert fast == dump()
+    assert storage._scalar_dict_body.__name__ == "<lambda>"
+    monkeypatch.undo()
+    body = storage._scalar_dict_body(coef, 0)
+    assert "{\n" + body + "\n}" == json.dumps(coef, indent=4, ensure_ascii=False)
+
+
 def test_storage_latest_skips_claimed_placeholder(tmp_path, monkeypatch):
     """A number claimed by a solve still writing (empty file) is not 'latest'."""
     from simplex_amd import storage
