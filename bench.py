@@ -102,7 +102,7 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=15.0,
                     help="budget of the CPU-baseline sample (0 disables)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles",
-                                                           "traffic_r05.json"))
+                                                           "traffic_r06.json"))
     return ap.parse_args()
 
 

@@ -155,6 +155,10 @@ struct spx_ctx {
   unsigned long long* gr_enter = nullptr;  // ENTER_REC x CHAIN_MAX_BLOCKS granules
   unsigned long long* gr_ratio = nullptr;  // RATIO_REC x CHAIN_MAX_BLOCKS granules
   size_t A_bytes = 0, gr_bytes = 0;
+  int epl_alloc = 0, rpl_alloc = 0;  // entering / ratio partial slots allocated
+  // row-transfer staging buffer kept between calls when small (transfer_rows)
+  double* stage = nullptr;
+  size_t stage_bytes = 0;
   int chain_mode = 0;      // 0: persistent chain when it fits, 1: launch per phase
   int chain_min_blocks = 0;
   // admission of the persistent chain (process-wide block budget per device):
@@ -1420,42 +1424,64 @@ int rp_recover(spx_ctx* ctx) {
 }
 
 int alloc_common(spx_ctx* ctx, int64_t m_local, int64_t N, int64_t m_global, int64_t row0) {
-  free_buffers(ctx);
-  ctx->m_local = m_local;
-  ctx->m_global = m_global;
-  ctx->row0 = row0;
-  ctx->N = N;
   const int pad = ctx->ld_pad >= 0 ? ctx->ld_pad : (m_local >= 4096 ? 256 : 0);
-  ctx->ld = std::max<int64_t>(64, round_up(m_local, 64)) + pad;
-  choose_geometry(ctx);
-  ctx->hist_cap = 1 << 20;
-  HIPC(hipSetDevice(ctx->device));
-  ctx->A_bytes = sizeof(double) * ctx->ld * N;
-  // (the buffers a row shard may export come from its pool, spx_ctx::pool)
-  const bool exportable = ctx->sharded && !ctx->loop;
-  if (exportable) {
-    if (const int rc = pool_take(ctx, POOL_TABLEAU, ctx->A_bytes, false,
-                                 reinterpret_cast<void**>(&ctx->A), &ctx->A_bytes))
-      return rc;
-  } else {
-    HIPC(hipMalloc(&ctx->A, ctx->A_bytes));
+  const int64_t ld = std::max<int64_t>(64, round_up(m_local, 64)) + pad;
+  // A single-GPU reload of the loaded shape keeps every buffer and only clears
+  // them again (round 6: the reference's user path solves small LPs one after
+  // another on a pooled context, and ~30 hipMalloc / hipFree pairs were most
+  // of a 0.5 ms load; tests/test_gpu_user_path.py).  Row shards always take
+  // the allocation path below (their exported buffers go through the pool).
+  bool reuse = !ctx->sharded && !ctx->loop && ctx->A && ctx->m_local == m_local &&
+               ctx->N == N && ctx->m_global == m_global && ctx->row0 == row0 && ctx->ld == ld;
+  if (reuse) {
+    choose_geometry(ctx);  // (knobs set since the last load may move the partial counts)
+    reuse = enter_part_len(ctx) <= ctx->epl_alloc && ratio_part_len(ctx) <= ctx->rpl_alloc;
   }
-  HIPC(hipMalloc(&ctx->obj, sizeof(double) * N));
-  HIPC(hipMalloc(&ctx->F, sizeof(double) * 2 * ctx->ld));
-  HIPC(hipMalloc(&ctx->P, sizeof(double) * N));
-  HIPC(hipMalloc(&ctx->list, sizeof(int) * N));
-  HIPC(hipMalloc(&ctx->basis, sizeof(int64_t) * std::max<int64_t>(1, m_global)));
-  HIPC(hipMalloc(&ctx->hist, sizeof(int64_t) * 2 * ctx->hist_cap));
-  HIPC(hipMalloc(&ctx->enter_part, sizeof(Key) * enter_part_len(ctx)));  // per wave / chain block
-  HIPC(hipMalloc(&ctx->ratio_part, sizeof(Key) * ratio_part_len(ctx)));
-  {
+  HIPC(hipSetDevice(ctx->device));
+  // shards: every rank's records, two parity halves and the window-end plane
+  // (peers write them over xGMI: uncached, so this GPU's L2 never serves a
+  // stale copy to the local polls; plain memory between virtual ranks)
+  // (+2 planes: the start handshake's arrivals and verdict word; shards also
+  // the IPC release plane and the owner-push inbox, spx_chain.hpp)
+  const size_t gq = sizeof(unsigned long long) *
+                    (ctx->sharded ? (size_t)shard_record_granules(N)
+                                  : (size_t)(HS_PLANE_1GPU + 2) * CHAIN_MAX_BLOCKS);
+  if (reuse) {
+    drop_graphs(ctx);
+    ctx->loaded = false;
+  } else {
+    free_buffers(ctx);
+    ctx->m_local = m_local;
+    ctx->m_global = m_global;
+    ctx->row0 = row0;
+    ctx->N = N;
+    ctx->ld = ld;
+    choose_geometry(ctx);
+    ctx->hist_cap = 1 << 20;
+    ctx->A_bytes = sizeof(double) * ctx->ld * N;
+    // (the buffers a row shard may export come from its pool, spx_ctx::pool)
+    const bool exportable = ctx->sharded && !ctx->loop;
+    if (exportable) {
+      if (const int rc = pool_take(ctx, POOL_TABLEAU, ctx->A_bytes, false,
+                                   reinterpret_cast<void**>(&ctx->A), &ctx->A_bytes))
+        return rc;
+    } else {
+      HIPC(hipMalloc(&ctx->A, ctx->A_bytes));
+    }
+    HIPC(hipMalloc(&ctx->obj, sizeof(double) * N));
+    HIPC(hipMalloc(&ctx->F, sizeof(double) * 2 * ctx->ld));
+    HIPC(hipMalloc(&ctx->P, sizeof(double) * N));
+    HIPC(hipMalloc(&ctx->list, sizeof(int) * N));
+    HIPC(hipMalloc(&ctx->basis, sizeof(int64_t) * std::max<int64_t>(1, m_global)));
+    HIPC(hipMalloc(&ctx->hist, sizeof(int64_t) * 2 * ctx->hist_cap));
+    ctx->epl_alloc = enter_part_len(ctx);
+    ctx->rpl_alloc = ratio_part_len(ctx);
+    HIPC(hipMalloc(&ctx->enter_part, sizeof(Key) * ctx->epl_alloc));  // per wave / chain block
+    HIPC(hipMalloc(&ctx->ratio_part, sizeof(Key) * ctx->rpl_alloc));
     // shared by both window sets: column tags, the window epoch, the fold words
     HIPC(hipMalloc(&ctx->wins[0].tag, sizeof(uint32_t) * N));
     HIPC(hipMalloc(&ctx->wins[0].epoch, sizeof(uint32_t)));
     HIPC(hipMalloc(&ctx->wins[0].fix, sizeof(int32_t) * 8));
-    HIPC(hipMemsetAsync(ctx->wins[0].tag, 0, sizeof(uint32_t) * N, ctx->stream));
-    HIPC(hipMemsetAsync(ctx->wins[0].epoch, 0, sizeof(uint32_t), ctx->stream));
-    HIPC(hipMemsetAsync(ctx->wins[0].fix, 0, sizeof(int32_t) * 8, ctx->stream));
     for (int x = 0; x < 2; ++x) {
       Window& w = ctx->wins[x];
       w.tag = ctx->wins[0].tag;
@@ -1471,29 +1497,8 @@ int alloc_common(spx_ctx* ctx, int64_t m_local, int64_t N, int64_t m_global, int
       HIPC(hipMalloc(&w.rec, sizeof(double) * RECW * N));
       HIPC(hipMalloc(&w.frt, sizeof(double) * KW * KW));
       HIPC(hipMalloc(&w.Pf, sizeof(double) * KW * N));
-      HIPC(hipMemsetAsync(w.Pf, 0, sizeof(double) * KW * N, ctx->stream));
-      HIPC(hipMemsetAsync(w.frt, 0, sizeof(double) * KW * KW, ctx->stream));
-      HIPC(hipMemsetAsync(w.nlist, 0, sizeof(int32_t), ctx->stream));
-      HIPC(hipMemsetAsync(w.rec, 0, sizeof(double) * RECW * N, ctx->stream));
-      HIPC(hipMemsetAsync(w.F, 0, sizeof(double) * KW * ctx->ld, ctx->stream));
-      HIPC(hipMemsetAsync(w.P, 0, sizeof(double) * KW * N, ctx->stream));
-      HIPC(hipMemsetAsync(w.made, 0, sizeof(int32_t) * KW, ctx->stream));
-      HIPC(hipMemsetAsync(w.r, 0, sizeof(int64_t) * KW, ctx->stream));
-      HIPC(hipMemsetAsync(w.c, 0, sizeof(int64_t) * KW, ctx->stream));
     }
-    ctx->wpar = 0;
-    ctx->last_fold = false;
-    const size_t ge = sizeof(unsigned long long) * ENTER_REC * CHAIN_MAX_BLOCKS;
-    // shards: every rank's records, two parity halves and the window-end plane
-    // (peers write them over xGMI: uncached, so this GPU's L2 never serves a
-    // stale copy to the local polls; plain memory between virtual ranks)
-    // (+2 planes: the start handshake's arrivals and verdict word)
-    // (+2 planes: the start handshake's arrivals and verdict word; shards also
-    // the IPC release plane and the owner-push inbox, spx_chain.hpp)
-    const size_t gq = sizeof(unsigned long long) *
-                      (ctx->sharded ? (size_t)shard_record_granules(N)
-                                    : (size_t)(HS_PLANE_1GPU + 2) * CHAIN_MAX_BLOCKS);
-    HIPC(hipMalloc(&ctx->gr_enter, ge));
+    HIPC(hipMalloc(&ctx->gr_enter, sizeof(unsigned long long) * ENTER_REC * CHAIN_MAX_BLOCKS));
     ctx->gr_bytes = gq;
     if (exportable) {
       if (const int rc = pool_take(ctx, POOL_RECORDS, gq, true,
@@ -1502,15 +1507,34 @@ int alloc_common(spx_ctx* ctx, int64_t m_local, int64_t N, int64_t m_global, int
     } else {
       HIPC(hipMalloc(&ctx->gr_ratio, gq));
     }
-    HIPC(hipMemsetAsync(ctx->gr_enter, 0, ge, ctx->stream));
-    HIPC(hipMemsetAsync(ctx->gr_ratio, 0, gq, ctx->stream));
+    if (ctx->sharded) {
+      ctx->gstride = round_up(PAYLOAD_HDR + (int64_t)sizeof(double) * N, 256);
+      HIPC(hipMalloc(&ctx->sendbuf, ctx->gstride));
+      HIPC(hipMalloc(&ctx->recvbuf, ctx->gstride * ctx->nranks));
+    }
   }
-  if (ctx->sharded) {
-    ctx->gstride = round_up(PAYLOAD_HDR + (int64_t)sizeof(double) * N, 256);
-    HIPC(hipMalloc(&ctx->sendbuf, ctx->gstride));
-    HIPC(hipMalloc(&ctx->recvbuf, ctx->gstride * ctx->nranks));
-    HIPC(hipMemsetAsync(ctx->sendbuf, 0, ctx->gstride, ctx->stream));
+  // every load starts from zeroed buffers, reused or new
+  HIPC(hipMemsetAsync(ctx->wins[0].tag, 0, sizeof(uint32_t) * N, ctx->stream));
+  HIPC(hipMemsetAsync(ctx->wins[0].epoch, 0, sizeof(uint32_t), ctx->stream));
+  HIPC(hipMemsetAsync(ctx->wins[0].fix, 0, sizeof(int32_t) * 8, ctx->stream));
+  for (int x = 0; x < 2; ++x) {
+    Window& w = ctx->wins[x];
+    HIPC(hipMemsetAsync(w.Pf, 0, sizeof(double) * KW * N, ctx->stream));
+    HIPC(hipMemsetAsync(w.frt, 0, sizeof(double) * KW * KW, ctx->stream));
+    HIPC(hipMemsetAsync(w.nlist, 0, sizeof(int32_t), ctx->stream));
+    HIPC(hipMemsetAsync(w.rec, 0, sizeof(double) * RECW * N, ctx->stream));
+    HIPC(hipMemsetAsync(w.F, 0, sizeof(double) * KW * ctx->ld, ctx->stream));
+    HIPC(hipMemsetAsync(w.P, 0, sizeof(double) * KW * N, ctx->stream));
+    HIPC(hipMemsetAsync(w.made, 0, sizeof(int32_t) * KW, ctx->stream));
+    HIPC(hipMemsetAsync(w.r, 0, sizeof(int64_t) * KW, ctx->stream));
+    HIPC(hipMemsetAsync(w.c, 0, sizeof(int64_t) * KW, ctx->stream));
   }
+  ctx->wpar = 0;
+  ctx->last_fold = false;
+  HIPC(hipMemsetAsync(ctx->gr_enter, 0, sizeof(unsigned long long) * ENTER_REC * CHAIN_MAX_BLOCKS,
+                      ctx->stream));
+  HIPC(hipMemsetAsync(ctx->gr_ratio, 0, gq, ctx->stream));
+  if (ctx->sharded) HIPC(hipMemsetAsync(ctx->sendbuf, 0, ctx->gstride, ctx->stream));
   HIPC(hipMemsetAsync(ctx->A, 0, sizeof(double) * ctx->ld * N, ctx->stream));
   HIPC(hipMemsetAsync(ctx->F, 0, sizeof(double) * 2 * ctx->ld, ctx->stream));
   HIPC(hipMemsetAsync(ctx->P, 0, sizeof(double) * N, ctx->stream));
@@ -1954,6 +1978,7 @@ int spx_destroy(spx_ctx* ctx) {
   if (ctx->h_poll) (void)hipHostFree(ctx->h_poll);
   if (ctx->h_stop) (void)hipHostFree(ctx->h_stop);
   dfree(ctx->d_peers);
+  dfree(ctx->stage);
   for (hipEvent_t ev : ctx->ev_poll)
     if (ev) (void)hipEventDestroy(ev);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
@@ -1971,8 +1996,24 @@ int transfer_rows(spx_ctx* ctx, double* host, int64_t nrows, int64_t cols, int64
   // grid's y limit)
   const int64_t chunk = std::min<int64_t>(
       65535 * 32, std::max<int64_t>(32, std::min<int64_t>(nrows, ((8 << 20) / cols + 31) / 32 * 32)));
+  // a staging buffer of at most STAGE_KEEP bytes stays with the context (the
+  // per-step snapshots of a small LP, round 6: a hipMalloc / hipFree pair per
+  // snapshot was most of its cost); larger ones are freed after the call
+  constexpr size_t STAGE_KEEP = (size_t)8 << 20;
+  const size_t need = sizeof(double) * chunk * cols;
   double* stage = nullptr;
-  HIPC(hipMalloc(&stage, sizeof(double) * chunk * cols));
+  const bool keep = need <= STAGE_KEEP;
+  if (keep) {
+    if (ctx->stage_bytes < need) {
+      dfree(ctx->stage);
+      ctx->stage_bytes = 0;
+      HIPC(hipMalloc(&ctx->stage, need));
+      ctx->stage_bytes = need;
+    }
+    stage = ctx->stage;
+  } else {
+    HIPC(hipMalloc(&stage, need));
+  }
   int rc = SPX_OK;
   for (int64_t i0 = 0; i0 < nrows && rc == SPX_OK; i0 += chunk) {
     const int64_t R = std::min(chunk, nrows - i0);
@@ -2001,7 +2042,7 @@ int transfer_rows(spx_ctx* ctx, double* host, int64_t nrows, int64_t cols, int64
       rc = SPX_E_HIP;
     }
   }
-  (void)hipFree(stage);
+  if (!keep) (void)hipFree(stage);
   return rc;
 }
 

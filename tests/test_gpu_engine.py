@@ -196,6 +196,41 @@ def test_graph_and_direct_and_chunks_agree(eng_cls):
         assert np.array_equal(o[3], outs[0][3])
 
 
+def test_reload_same_shape_keeps_buffers_bit_exact(eng_cls):
+    """One context, many loads (round 6: a reload of the loaded shape keeps the
+    device buffers and only clears them, the pooled contexts of the user
+    path).  LPs of one shape with other seeds, both rules, windows of 8 and 24
+    and single pivots, an unfinished solve before each reload (its window
+    state, records and history must not leak into the next load), another
+    shape in between and back: every run equals the oracle's run from its own
+    load."""
+    from simplex_amd import synth
+    shapes = [(120, 200, 1, "dense"), (120, 200, 2, "dense"), (120, 200, 3, "degenerate"),
+              (64, 100, 4, "dense"), (120, 200, 5, "degenerate"), (120, 200, 6, "dense"),
+              (700, 900, 7, "dense"), (700, 900, 8, "dense")]
+    with eng_cls(0) as eng:
+        for k, (m, n, seed, kind) in enumerate(shapes):
+            rule = "bland" if kind == "degenerate" else "dantzig"
+            T, basis = synth.full_tableau(kind, m, n, seed)
+            ref, rb = T.copy(), basis.copy()
+            st, hist = O.solve_tableau(ref, rb, rule=rule, max_iters=3000)
+            window = (0, 8, 24)[k % 3]
+            # an unfinished windowed solve of the same data first, then the reload
+            eng.set_window(16)
+            eng.load(T, basis)
+            eng.solve(rule=rule, max_iters=37)
+            eng.set_window(window)
+            eng.load(T, basis)
+            for q in range(min(3, len(hist))):
+                assert eng.pivot(rule=rule) == hist[q]
+            res = eng.solve(rule=rule, max_iters=3000 - min(3, len(hist)))
+            assert res.status == st, (k, res.status, st)
+            assert [tuple(h) for h in eng.history().tolist()] == hist, k
+            assert np.array_equal(eng.tableau(), ref), k
+            assert np.array_equal(eng.basis(), rb), k
+        eng.set_window(0)
+
+
 def test_iteration_limit_and_resume(eng_cls):
     from simplex_amd import synth
     T, basis = synth.full_tableau("dense", 64, 96, 7)
