@@ -1447,7 +1447,11 @@ int alloc_common(spx_ctx* ctx, int64_t m_local, int64_t N, int64_t m_global, int
                     (ctx->sharded ? (size_t)shard_record_granules(N)
                                   : (size_t)(HS_PLANE_1GPU + 2) * CHAIN_MAX_BLOCKS);
   if (reuse) {
-    drop_graphs(ctx);
+    // The captured graphs stay too: their launches name the same buffers and
+    // sizes, everything a call changes is read from device memory (Params /
+    // State, written by call_begin_kernel), and every knob that changes a
+    // launch drops them in its setter.  (A small LP's spx_solve spent ~0.4 ms
+    // capturing its 32-pivot graph after every reload.)
     ctx->loaded = false;
   } else {
     free_buffers(ctx);
@@ -1513,31 +1517,43 @@ int alloc_common(spx_ctx* ctx, int64_t m_local, int64_t N, int64_t m_global, int
       HIPC(hipMalloc(&ctx->recvbuf, ctx->gstride * ctx->nranks));
     }
   }
-  // every load starts from zeroed buffers, reused or new
-  HIPC(hipMemsetAsync(ctx->wins[0].tag, 0, sizeof(uint32_t) * N, ctx->stream));
-  HIPC(hipMemsetAsync(ctx->wins[0].epoch, 0, sizeof(uint32_t), ctx->stream));
-  HIPC(hipMemsetAsync(ctx->wins[0].fix, 0, sizeof(int32_t) * 8, ctx->stream));
+  // every load starts from zeroed buffers, reused or new: the tableau by a
+  // fill, the rest in one launch (zero_spans_kernel)
+  ZeroSpans z{};
+  uint64_t most = 0;
+  auto span = [&](void* ptr, size_t bytes) {
+    z.p[z.n] = static_cast<uint32_t*>(ptr);
+    z.words[z.n] = bytes / 4;  // (every size here is a multiple of 4 B)
+    most = std::max<uint64_t>(most, bytes / 16);
+    ++z.n;
+  };
+  span(ctx->wins[0].tag, sizeof(uint32_t) * N);
+  span(ctx->wins[0].epoch, sizeof(uint32_t));
+  span(ctx->wins[0].fix, sizeof(int32_t) * 8);
   for (int x = 0; x < 2; ++x) {
     Window& w = ctx->wins[x];
-    HIPC(hipMemsetAsync(w.Pf, 0, sizeof(double) * KW * N, ctx->stream));
-    HIPC(hipMemsetAsync(w.frt, 0, sizeof(double) * KW * KW, ctx->stream));
-    HIPC(hipMemsetAsync(w.nlist, 0, sizeof(int32_t), ctx->stream));
-    HIPC(hipMemsetAsync(w.rec, 0, sizeof(double) * RECW * N, ctx->stream));
-    HIPC(hipMemsetAsync(w.F, 0, sizeof(double) * KW * ctx->ld, ctx->stream));
-    HIPC(hipMemsetAsync(w.P, 0, sizeof(double) * KW * N, ctx->stream));
-    HIPC(hipMemsetAsync(w.made, 0, sizeof(int32_t) * KW, ctx->stream));
-    HIPC(hipMemsetAsync(w.r, 0, sizeof(int64_t) * KW, ctx->stream));
-    HIPC(hipMemsetAsync(w.c, 0, sizeof(int64_t) * KW, ctx->stream));
+    span(w.Pf, sizeof(double) * KW * N);
+    span(w.frt, sizeof(double) * KW * KW);
+    span(w.nlist, sizeof(int32_t));
+    span(w.rec, sizeof(double) * RECW * N);
+    span(w.F, sizeof(double) * KW * ctx->ld);
+    span(w.P, sizeof(double) * KW * N);
+    span(w.made, sizeof(int32_t) * KW);
+    span(w.r, sizeof(int64_t) * KW);
+    span(w.c, sizeof(int64_t) * KW);
   }
   ctx->wpar = 0;
   ctx->last_fold = false;
-  HIPC(hipMemsetAsync(ctx->gr_enter, 0, sizeof(unsigned long long) * ENTER_REC * CHAIN_MAX_BLOCKS,
-                      ctx->stream));
-  HIPC(hipMemsetAsync(ctx->gr_ratio, 0, gq, ctx->stream));
-  if (ctx->sharded) HIPC(hipMemsetAsync(ctx->sendbuf, 0, ctx->gstride, ctx->stream));
+  span(ctx->gr_enter, sizeof(unsigned long long) * ENTER_REC * CHAIN_MAX_BLOCKS);
+  span(ctx->gr_ratio, gq);
+  if (ctx->sharded) span(ctx->sendbuf, ctx->gstride);
+  span(ctx->F, sizeof(double) * 2 * ctx->ld);
+  span(ctx->P, sizeof(double) * N);
+  static_assert(3 + 2 * 9 + 5 <= ZERO_SPANS_MAX, "zero spans");
+  const unsigned gx = (unsigned)std::min<uint64_t>(1024, std::max<uint64_t>(1, (most + BLK - 1) / BLK));
+  hipLaunchKernelGGL(zero_spans_kernel, dim3(gx, (unsigned)z.n), dim3(BLK), 0, ctx->stream, z);
+  HIPC(hipGetLastError());
   HIPC(hipMemsetAsync(ctx->A, 0, sizeof(double) * ctx->ld * N, ctx->stream));
-  HIPC(hipMemsetAsync(ctx->F, 0, sizeof(double) * 2 * ctx->ld, ctx->stream));
-  HIPC(hipMemsetAsync(ctx->P, 0, sizeof(double) * N, ctx->stream));
   std::memset(ctx->h_st, 0, sizeof(State));
   ctx->h_st->status = ST_RUNNING;
   ctx->h_st->forced_c = -1;
@@ -2206,7 +2222,7 @@ int spx_solve(spx_ctx* ctx, const spx_opts* opts, spx_result* res) {
   const int chunk =
       ctx->win_k ? ctx->win_k * ctx->graph_windows : (o->chunk > 0 ? o->chunk : 32);
   const bool use_graph = o->use_graph != 0 && !ctx->loop && !ctx->time_chain;
-  if (use_graph) {
+  if (use_graph && ctx->win_k) {
     rc = build_graphs_all(ctx, chunk);
     if (rc) return rc;
   }
@@ -2214,13 +2230,18 @@ int spx_solve(spx_ctx* ctx, const spx_opts* opts, spx_result* res) {
   // Chunk i+1 is enqueued before chunk i's status is read (a pinned State copy
   // per chunk, polled one chunk behind), so the stream never drains while the
   // host looks.  The chunk after the terminating one only runs early-exiting
-  // launches: every kernel checks the device status first.
+  // launches: every kernel checks the device status first.  Single pivots
+  // ramp up: chunks of 4, 8, 16 pivots launched directly, then the graph of
+  // `chunk` (round 6: a textbook LP stops after a few pivots, and two graphs of
+  // 32 pivots were ~0.3 ms of early-exiting launches on its user path).
   auto launch_chunk = [&](int64_t i) -> int {
-    if (use_graph) {
-      const int r = launch_graph(ctx, chunk);
+    const int ramp = ctx->win_k ? chunk : (int)std::min<int64_t>(chunk, (int64_t)4 << std::min<int64_t>(i, 8));
+    if (use_graph && ramp == chunk) {
+      int r = ctx->win_k ? SPX_OK : build_graph(ctx, chunk);  // (cached after the first)
+      if (!r) r = launch_graph(ctx, chunk);
       if (r) return r;
     } else {
-      const int r = enqueue_pivots(ctx, chunk, 0);
+      const int r = enqueue_pivots(ctx, ramp, 0);
       if (r) return r;
     }
     HIPC(hipMemcpyAsync(ctx->h_poll + (i & 1), ctx->st, sizeof(State), hipMemcpyDeviceToHost,

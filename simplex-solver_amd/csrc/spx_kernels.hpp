@@ -41,6 +41,29 @@ namespace spx {
 constexpr int BLK = 256;  // threads per workgroup (4 wave64)
 constexpr int NWAVE = BLK / 64;
 
+// The load's zeroing of a context's small buffers in one launch (spx_load /
+// spx_load_rows, alloc_common): span y of the list is cleared by the blocks
+// of grid row y, 16-B stores over its 16-B-aligned body (every span starts at
+// a hipMalloc'd, 256-B-aligned address) and 4-B stores over the rest.  Replaces
+// ~25 fill launches per load (round 6: a textbook LP's load was mostly those).
+constexpr int ZERO_SPANS_MAX = 32;
+struct ZeroSpans {
+  uint32_t* p[ZERO_SPANS_MAX];
+  uint64_t words[ZERO_SPANS_MAX];  // 4-B words per span
+  int n;
+};
+__global__ __launch_bounds__(256) void zero_spans_kernel(ZeroSpans z) {
+  const int s = blockIdx.y;
+  if (s >= z.n) return;
+  uint32_t* p = z.p[s];
+  const uint64_t w = z.words[s], w4 = w / 4;
+  const uint64_t t0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint64_t step = (uint64_t)gridDim.x * blockDim.x;
+  uint4* q = reinterpret_cast<uint4*>(p);
+  for (uint64_t i = t0; i < w4; i += step) q[i] = make_uint4(0u, 0u, 0u, 0u);
+  for (uint64_t i = w4 * 4 + t0; i < w; i += step) p[i] = 0u;
+}
+
 // Row-major <-> column-major transposes of the boundary (spx_load_rows /
 // spx_get_tableau with SPX_ROW_MAJOR): 32 x 32 tiles through LDS (a padded
 // row, so the column reads do not share a bank), 32 x 8 threads, so both the
