@@ -848,14 +848,14 @@ __global__ __launch_bounds__(BLK) void flush_lds_kernel(double* __restrict__ A, 
 // whose last leaving slot is L ends at p_L[j] followed by the later pivots'
 // msub updates (their leaving rows differ from r).  One thread per column.
 // ---------------------------------------------------------------------------
-// fix_rows<K, TPB>: the body of row_fix_kernel -- the records kr0, kr0 +
-// stride, ... of `win`, one per thread at a time (the first loaded before the
-// list length is known); also run by the fold blocks of chain_kernel<.., true>
-// on the previous window's set (INCHAIN: no probe stamps).
-template <int K, int TPB, bool INCHAIN = false>
+// fix_rows<K, TPB>: the body of row_fix_kernel -- record kr of `win`, one per
+// thread (loaded before the list length is known).  (Round 6's first fold form
+// ran this in a loop over records from extra chain blocks; that form lost, and
+// the loop with its anti-hoisting index cost the standalone kernel 13.3 -> 15.8
+// us per window, so the one-record body is back.)
+template <int K, int TPB>
 __device__ __forceinline__ void fix_rows(double* A, int64_t ld, int64_t m_local, int64_t row0,
-                                         int64_t N, const Window& win, int npiv, int64_t kr0,
-                                         int64_t stride) {
+                                         int64_t N, const Window& win, int npiv, int64_t kr) {
   __shared__ double fr[K][K];  // fr[L][s] = f_s[r_L]
   __shared__ int64_t rows[K];
   __shared__ int lastL[K];
@@ -872,10 +872,9 @@ __device__ __forceinline__ void fix_rows(double* A, int64_t ld, int64_t m_local,
   // and ~2.5 us to issue the scattered stores (the stores themselves: ~1.4
   // us).  64-thread blocks and the K chains interleaved slot-major measured
   // 14.3-14.9 us, not kept.)
-  int64_t kr = kr0;
-  int64_t kc = kr < N ? kr : N - 1;  // the record buffer holds N records
+  const int64_t kc = kr < N ? kr : N - 1;  // the record buffer holds N records
   const int nl = *win.nlist;
-  int64_t hdr = reinterpret_cast<const int64_t*>(win.rec)[kc * RECW];
+  const int64_t hdr = reinterpret_cast<const int64_t*>(win.rec)[kc * RECW];
   double p[K];
 #pragma unroll
   for (int s = 0; s < K; ++s) p[s] = win.rec[kc * RECW + 2 + s];
@@ -884,7 +883,7 @@ __device__ __forceinline__ void fix_rows(double* A, int64_t ld, int64_t m_local,
     made_sh[t] = t < npiv ? win.made[t] : 0;
   }
   __syncthreads();
-  if constexpr (!INCHAIN) SPX_PROBE(K + 1, 0, 1, hdr != 12345 && p[K - 1] != 12345.678);
+  SPX_PROBE(K + 1, 0, 1, hdr != 12345 && p[K - 1] != 12345.678);
   // made slots of this window: a prefix of its npiv launched ones
   int madeK = 0;
 #pragma unroll
@@ -912,37 +911,20 @@ __device__ __forceinline__ void fix_rows(double* A, int64_t ld, int64_t m_local,
     const int x = t + u * TPB;
     if (x < K * K) fr[x / K][x % K] = fv[u];
   }
-  if constexpr (!INCHAIN) SPX_PROBE(K + 1, 0, 2, fv[0] != 12345.678);  // round 2 arrived
+  SPX_PROBE(K + 1, 0, 2, fv[0] != 12345.678);  // round 2 arrived
   __syncthreads();
-  if constexpr (!INCHAIN) SPX_PROBE(K + 1, 1, 2, true);  // lastL and the barrier done
-  if (madeK == 0) return;
-#pragma unroll 1
-  while (kr < nl) {
-    const int64_t j = hdr & 0xffffffffll;
-    const bool fast = (hdr >> 32) == 0;  // not SPECIAL / ZERO: the flush's plain msub chain
-    // (an opaque 0 in the LDS indices: the loop-invariant fr / rows / lastL
-    // reads would otherwise be hoisted out of the record loop, K^2 values
-    // held in registers)
-    int z = 0;
-    asm volatile("" : "+v"(z));
-    const double* frz = &fr[0][0] + z;
-    if (fast) {
+  SPX_PROBE(K + 1, 1, 2, true);  // lastL and the barrier done
+  const int64_t j = hdr & 0xffffffffll;
+  const bool fast = (hdr >> 32) == 0;  // not SPECIAL / ZERO: the flush's plain msub chain
+  if (madeK == 0 || kr >= nl || !fast) return;
 #pragma unroll
-      for (int L = 0; L < K; ++L) {
-        const int64_t rL = rows[L + z];
-        if (L >= madeK || !lastL[L + z] || rL < 0 || rL >= m_local) continue;  // not ours
-        double x = p[L];  // p_L[j], then the later slots
+  for (int L = 0; L < K; ++L) {
+    if (L >= madeK || !lastL[L] || rows[L] < 0 || rows[L] >= m_local) continue;  // not ours
+    double x = p[L];  // p_L[j], then the later slots
 #pragma unroll
-        for (int s = L + 1; s < K; ++s)
-          if (s < madeK) x = msub(x, frz[L * K + s], p[s]);
-        __builtin_nontemporal_store(x, A + j * ld + rL);  // scattered 8-B writes: no L2 allocate
-      }
-    }
-    kr += stride;
-    if (kr >= nl) break;
-    hdr = reinterpret_cast<const int64_t*>(win.rec)[kr * RECW];
-#pragma unroll
-    for (int s = 0; s < K; ++s) p[s] = win.rec[kr * RECW + 2 + s];
+    for (int s = L + 1; s < K; ++s)
+      if (s < madeK) x = msub(x, fr[L][s], p[s]);
+    __builtin_nontemporal_store(x, A + j * ld + rows[L]);  // scattered 8-B writes: no L2 allocate
   }
 }
 
@@ -984,8 +966,7 @@ __global__ __launch_bounds__(TPB) void row_fix_kernel(double* __restrict__ A, in
   } else {
     if (blockIdx.x == 0 && t == 0) win.fix[win.sid] = 0;
   }
-  fix_rows<K, TPB>(A, ld, m_local, row0, N, win, npiv, (int64_t)blockIdx.x * TPB + t,
-                   (int64_t)gridDim.x * TPB);
+  fix_rows<K, TPB>(A, ld, m_local, row0, N, win, npiv, (int64_t)blockIdx.x * TPB + t);
 #ifdef SPX_PHASE_TIMING
   SPX_PROBE(K + 1, 0, 3, true);  // stores issued
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
