@@ -560,7 +560,9 @@ def main():
     between = every - 1
     every = f"every {every}th"
     window = (f"timed region: HIP events on the engine stream around {every} {what}, "
-              f"launched directly" + ("; of the windows in between, runs of 4 replay one "
+              f"launched directly" + (" (the flush's start / stop events ride in its own launch, "
+                                      "hipExtLaunchKernel: its dispatch span, as rocprofv3 "
+                                      "measures it)" if K else "") + ("; of the windows in between, runs of 4 replay one "
                                       "hipGraph (SPX_GRAPH_WINDOWS), the rest are launched "
                                       "directly" if (use_graph and K and between) else ""))
     avg_ms = ms_tot / launches

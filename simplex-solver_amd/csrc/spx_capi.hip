@@ -16,6 +16,7 @@
 // has no MINLOC op for) and the winner's row as the pivot row (the owner's
 // broadcast, without a host-known root).
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 #include <rccl/rccl.h>
 #include <errno.h>
 #include <fcntl.h>
@@ -1060,20 +1061,34 @@ int enqueue_window_t(spx_ctx* ctx, int npiv, bool time_flush) {
     const int rc = record_event(ctx, ec->second);
     if (rc) return rc;
   }
+  // A timed flush outside a capture carries its events in its own launch
+  // (hipExtLaunchKernel: the events take the kernel's dispatch start / end
+  // timestamps, the span rocprofv3 reports, and no event packets sit between
+  // the chain and the flush); inside a capture, event-record nodes around it.
   std::pair<hipEvent_t, hipEvent_t>* e = nullptr;
+  bool ext = false;
   if (time_flush) {
     int rc = next_event_pair(ctx, ctx->ev, ctx->ev_used, &e);
-    if (!rc) rc = record_event(ctx, e->first);
     if (rc) return rc;
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    HIPC(hipStreamIsCapturing(ctx->stream, &cs));
+    ext = cs != hipStreamCaptureStatusActive;
+    if (!ext && (rc = record_event(ctx, e->first))) return rc;
   }
   auto go = [&](auto kern, int rt, int threads = BLK) {
     const int rch = flush_rch(ctx, rt);
     const int G = flush_groups(ctx, (const void*)kern, rch, threads);
     ctx->last_flush_G = G;
     ctx->last_flush_rch = rch;
-    hipLaunchKernelGGL(kern, dim3(rch * G), dim3(threads), 0, ctx->stream, ctx->A, ctx->ld,
-                       ctx->m_local, ctx->row0, ctx->N, win, npiv, rch, G, ctx->prm,
-                       ctx->st, ctx->flush_map | ctx->flush_tail << 8);
+    if (ext)
+      hipExtLaunchKernelGGL(kern, dim3(rch * G), dim3(threads), 0, ctx->stream, e->first,
+                            e->second, 0, ctx->A, ctx->ld, ctx->m_local, ctx->row0, ctx->N, win,
+                            npiv, rch, G, (const Params*)ctx->prm, ctx->st,
+                            ctx->flush_map | ctx->flush_tail << 8);
+    else
+      hipLaunchKernelGGL(kern, dim3(rch * G), dim3(threads), 0, ctx->stream, ctx->A, ctx->ld,
+                         ctx->m_local, ctx->row0, ctx->N, win, npiv, rch, G, ctx->prm,
+                         ctx->st, ctx->flush_map | ctx->flush_tail << 8);
   };
   const bool nts = (ctx->elim_nt & 2) != 0;
   // the LDS-DMA ring of 12 columns per wave over the window's compacted
@@ -1083,7 +1098,7 @@ int enqueue_window_t(spx_ctx* ctx, int npiv, bool time_flush) {
     nts ? go(flush_lds_kernel<KMAX, 12, true, true>, 2) : go(flush_lds_kernel<KMAX, 12, false, true>, 2);
   else
     nts ? go(flush_lds_kernel<KMAX, 12, true>, 2) : go(flush_lds_kernel<KMAX, 12, false>, 2);
-  if (e) {
+  if (e && !ext) {
     const int rc = record_event(ctx, e->second);
     if (rc) return rc;
   }
