@@ -2250,7 +2250,8 @@ int spx_solve(spx_ctx* ctx, const spx_opts* opts, spx_result* res) {
   // `chunk` (round 6: a textbook LP stops after a few pivots, and two graphs of
   // 32 pivots were ~0.3 ms of early-exiting launches on its user path).
   auto launch_chunk = [&](int64_t i) -> int {
-    const int ramp = ctx->win_k ? chunk : (int)std::min<int64_t>(chunk, (int64_t)4 << std::min<int64_t>(i, 8));
+    const int64_t r4 = (int64_t)4 << std::min<int64_t>(i, 24);
+    const int ramp = ctx->win_k || r4 >= chunk ? chunk : (int)r4;
     if (use_graph && ramp == chunk) {
       int r = ctx->win_k ? SPX_OK : build_graph(ctx, chunk);  // (cached after the first)
       if (!r) r = launch_graph(ctx, chunk);

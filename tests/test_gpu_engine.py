@@ -185,8 +185,11 @@ def test_graph_and_direct_and_chunks_agree(eng_cls):
     from simplex_amd import synth
     T, basis = synth.full_tableau("dense", 200, 300, 11)
     outs = []
+    # (single-pivot solves ramp their chunks 4, 8, 16, ... up to `chunk`, then
+    # replay its graph: chunk 100 ramps through 64 first)
     for kw in (dict(use_graph=True, chunk=32), dict(use_graph=False, chunk=8),
-               dict(use_graph=True, chunk=1), dict(use_graph=True, chunk=7)):
+               dict(use_graph=True, chunk=1), dict(use_graph=True, chunk=7),
+               dict(use_graph=True, chunk=100), dict(use_graph=False, chunk=100)):
         with eng_cls(0) as eng:
             eng.load(T, basis)
             res = eng.solve(**kw)
