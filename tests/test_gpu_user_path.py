@@ -278,7 +278,7 @@ def test_user_path_stage_times(out_dir, monkeypatch):
     config 2; the GPU path's reports equal the stand-in's."""
     cases = [("config 1 (3 vars, test_visualization_integration.py:417-444)", CONFIG1, 20),
              ("load LP (Wyndor, test_performance_load.py:31-38)", WYNDOR, 20),
-             ("config 2 (1024 x 2048 dense, text API)", config2_wrapper(), 2)]
+             ("config 2 (1024 x 2048 dense, text API)", config2_wrapper(), 1)]
     out = []
     for name, wrap, reps in cases:
         row = {"workload": name}
