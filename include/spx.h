@@ -164,6 +164,12 @@ int spx_peer_debug(spx_ctx* ctx, uint64_t* out, int n);
  * exported buffer is never freed before spx_destroy, so out[0] == out[2].
  * n >= 3. */
 int spx_peer_pool_debug(spx_ctx* ctx, uint64_t* out, int n);
+/* Diagnostic (round 6): the device groups of the imported peer chain (ranks
+ * sharing a GPU; each group settles its own start handshake, then waits for
+ * the other groups' verdicts), this rank's group and its member count.
+ * SPX_PEER_GROUP_TAG (a test hook, read at spx_peer_export) splits ranks of
+ * one GPU into groups.  SPX_E_STATE before an import. */
+int spx_peer_groups(spx_ctx* ctx, int* ngroups, int* group, int* members);
 
 /* ---- data in / out ------------------------------------------------------- */
 /* Load a full tableau of `rows` = m+1 rows (objective row LAST) and `cols` = N

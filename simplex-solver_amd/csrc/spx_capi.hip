@@ -1832,6 +1832,15 @@ int spx_peer_export(spx_ctx* ctx, void* out, int64_t cap) {
   b.N = ctx->N;
   b.m_global = ctx->m_global;
   HIPC(hipDeviceGetPCIBusId(b.bus, (int)sizeof(b.bus) - 1, ctx->device));
+  // test hook (round 6): SPX_PEER_GROUP_TAG=x makes this rank's device key
+  // "<bus id>#x", so ranks on ONE GPU with different tags form different
+  // device groups -- each its own start handshake, then the cross-group
+  // verdict wait that ranks on different GPUs run (chain_start), which one
+  // GPU can then execute.  The caller keeps all groups' blocks within the CUs.
+  if (const char* tag = std::getenv("SPX_PEER_GROUP_TAG")) {
+    const size_t n = strnlen(b.bus, sizeof(b.bus));
+    std::snprintf(b.bus + n, sizeof(b.bus) - n, "#%s", tag);
+  }
   if (!ctx->n_cu) ctx->n_cu = device_cus(ctx->device);
   b.n_cu = ctx->n_cu;
   b.chain_mode = ctx->chain_mode;
@@ -2771,6 +2780,18 @@ int spx_peer_pool_debug(spx_ctx* ctx, uint64_t* out, int n) {
   out[0] = ctx->ever_exported.size();
   out[1] = ctx->pool.size();
   out[2] = held;
+  return SPX_OK;
+}
+
+int spx_peer_groups(spx_ctx* ctx, int* ngroups, int* group, int* members) {
+  if (!ctx || !ngroups || !group || !members) return SPX_E_ARG;
+  if (!ctx->peer_ok) {
+    ctx->err = "spx_peer_groups: no imported peer chain";
+    return SPX_E_STATE;
+  }
+  *ngroups = ctx->peers.ngroups;
+  *group = ctx->peers.group;
+  *members = ctx->peer_same_dev;
   return SPX_OK;
 }
 

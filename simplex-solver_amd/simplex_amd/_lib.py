@@ -116,6 +116,8 @@ SIGNATURES = {
     "spx_get_peer_push": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_int)]),
     "spx_peer_debug": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_uint64), ctypes.c_int]),
     "spx_peer_pool_debug": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_uint64), ctypes.c_int]),
+    "spx_peer_groups": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int),
+                                       ctypes.POINTER(ctypes.c_int)]),
     "spx_get_chain_stats": (ctypes.c_int, [_P, _LP]),
     "spx_set_chain_handshake": (ctypes.c_int, [_P, _I64]),
     "spx_chain_shm_path": (ctypes.c_int, [ctypes.c_int, ctypes.c_char_p, ctypes.c_int]),

@@ -147,6 +147,13 @@ class ShardedTableau(DeviceTableau):
         self._check(self._lib.spx_peer_pool_debug(self._ctx, out, 3), "spx_peer_pool_debug")
         return {"exported": out[0], "pooled": out[1], "held": out[2]}
 
+    def peer_groups(self) -> dict:
+        """Diagnostic: the imported peer chain's device groups (spx_peer_groups)."""
+        g, me, n = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        self._check(self._lib.spx_peer_groups(self._ctx, ctypes.byref(g), ctypes.byref(me),
+                                              ctypes.byref(n)), "spx_peer_groups")
+        return {"groups": g.value, "group": me.value, "members": n.value}
+
     @classmethod
     def from_env(cls, device: int | None = None, group=None) -> "ShardedTableau":
         import torch.distributed as dist

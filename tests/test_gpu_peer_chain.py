@@ -494,6 +494,7 @@ def test_peer_chain_four_processes_config3_width_256_threads(push):
     assert "fixture match True" in out and "chain reruns per rank" in out
     blocks = [int(x) for x in re.findall(r"chain blocks (\d+) pivots = fixture True", out)]
     assert blocks == [64] * 4, blocks
+    assert "rank 0: device groups 1 (this rank's: 0, 4 member(s))" in out
 
 
 @pytest.mark.timeout(600)
@@ -576,3 +577,39 @@ def test_full_pool_falls_back_to_rccl_on_a_comm_shard():
             st, hist = O.solve_tableau(Tf, bf, max_iters=30)
             assert res.status == st and [tuple(x) for x in s.history().tolist()] == hist
             assert np.array_equal(s.tableau()[:-1], Tf[:-1])
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("args", [
+    # 2 groups, pull and push, a solve to the end
+    ["--rows", "600", "--cols", "900", "--window", "8"],
+    ["--rows", "512", "--cols", "2048", "--window", "24", "--pivots", "101", "--push"],
+    # forced handshake aborts (every 3rd window) and a drain 0.6 s late: the
+    # groups' verdicts must agree on every aborted and every run window
+    ["--rows", "300", "--cols", "500", "--window", "4", "--pivots", "400",
+     "--abort-every", "3", "--run-pivots", "--late-drain", "0.6"],
+], ids=["solve", "push", "aborts_late_drain"])
+def test_peer_chain_device_groups_on_one_gpu(args):
+    """The start handshake of ranks on DIFFERENT GPUs (device groups: each
+    group settles its own arrivals, then waits for every other group's verdict
+    word with system-scope loads, DESIGN.md §4b "Residency") has run only in
+    the CPU model, since every hardware test put all ranks in one group.
+    SPX_PEER_GROUP_TAG (--fake-groups) gives each of two processes on GPU 0
+    its own group, so this path executes: bit-exact with the oracle, forced
+    aborts and a late drain included."""
+    out = _peer_run(2, args + ["--fake-groups"])
+    assert "RCCL_RANKS_CHECK PASS" in out
+    for q in range(2):
+        assert f"rank {q}: device groups 2 (this rank's: {q}, 1 member(s))" in out, out[-3000:]
+
+
+@pytest.mark.timeout(600)
+def test_peer_chain_four_device_groups_config3_width():
+    """Four ranks, four device groups on GPU 0 (4 x 64 blocks = every CU): the
+    config-3 tableau row-sharded 4 x 2048, 10 windows, pinned to the fixture."""
+    out = _peer_run(4, ["--rows", "8192", "--cols", "8192", "--seed", "20251205", "--window",
+                        "24", "--pivots", "240", "--chain", "2", "--fixture", "config3",
+                        "--fake-groups"])
+    assert "fixture match True" in out
+    for q in range(4):
+        assert f"rank {q}: device groups 4 (this rank's: {q}, 1 member(s))" in out, out[-3000:]

@@ -24,6 +24,9 @@ assembled tableau's SHA-256 checkpoint after --pivots) instead of running the
 oracle here (config 3 is 1 GB).  --ipc-log: print every rank's exported
 addresses, IPC handle digests and mapped peer pointers per load (DESIGN.md
 §5c); --no-solve skips the pivots (the IPC diagnostic alone).
+--fake-groups: every rank its own device group although all share GPU 0
+(SPX_PEER_GROUP_TAG), so the start handshake runs the cross-group verdict
+wait of ranks on different GPUs (keep all ranks' blocks within the CUs).
 --run-pivots: enqueue the pivots with spx_run_pivots (no host wait) and drain
 with spx_sync, instead of spx_solve; --late-drain S: the last rank sleeps S
 seconds before its drain (a window aborted at its start handshake is rerun at
@@ -62,6 +65,9 @@ def main():
                     help="force a start-handshake abort of every k-th window (test hook)")
     ap.add_argument("--run-pivots", action="store_true")
     ap.add_argument("--late-drain", type=float, default=0.0)
+    ap.add_argument("--fake-groups", action="store_true",
+                    help="each rank its own device group (SPX_PEER_GROUP_TAG=rank): the "
+                         "multi-GPU handshake's cross-group verdict wait on one GPU")
     ap.add_argument("--end-no-import", default="",
                     help="after the checked LPs, reload these sizes WITHOUT a peer import "
                          "(no pivots), check no exported buffer was freed, time the destroy")
@@ -69,6 +75,8 @@ def main():
     dist.init_process_group("gloo")
     rank, world = dist.get_rank(), dist.get_world_size()
     local = int(os.environ.get("LOCAL_RANK", rank))
+    if a.fake_groups:
+        os.environ["SPX_PEER_GROUP_TAG"] = str(rank)
     from simplex_amd import dist as sdist, synth
     dev = 0 if a.same_device else local
     sizes = [(a.rows, a.cols)] + [tuple(int(x) for x in z.split("x"))
@@ -109,6 +117,10 @@ def main():
                       f"mapped A {[hex(x) for x in d.get('peer_A', [])]} records "
                       f"{[hex(x) for x in d.get('peer_records', [])]}", flush=True)
             blocks = s.chain_blocks()
+            if a.peer and blocks > 0 and rows == sizes[0][0]:
+                g = s.peer_groups()
+                print(f"rank {rank}: device groups {g['groups']} (this rank's: {g['group']}, "
+                      f"{g['members']} member(s))", flush=True)
             if a.no_solve:
                 runs.append(None)
                 continue
