@@ -226,8 +226,10 @@ int spx_pivot_at(spx_ctx* ctx, int64_t r, int64_t c);
  * rank catches up with at once (tested with 0.6 s and 2.5 s lags on one
  * GPU).  The early ranks give up with SPX_E_STATE only after rerunning for 30
  * s (SPX_PEER_RERUN_S; round 5: after 16 aborts, ~1.7 s); ranks on different
- * GPUs still end in ST_FAULT after the ~4 s wait for the other GPUs'
- * verdicts (a verdict, once given, cannot be taken back consistently).  bench.py and dist.py drain every rank right after the
+ * GPUs (device groups) no longer fault after a ~4 s wait for the other
+ * GPUs' verdicts: a group still undecided after the handshake bound is
+ * decided ABORT by a compare-and-swap on its verdict word (round 6), so every
+ * group aborts that window and reruns it.  bench.py and dist.py drain every rank right after the
  * call, behind a barrier.  (2) The call's persistent-chain admission
  * (spx_set_chain_budget) is held until that drain, or until another call or
  * admission decision of this process sees the call's work complete; a

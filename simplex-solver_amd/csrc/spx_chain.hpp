@@ -400,14 +400,26 @@ __device__ __forceinline__ int chain_start(const gu64* arr, int nslots, int B, u
   v = __shfl(v, 0, 64);
   if (v != 1u) return 1;
   if (pe == nullptr || pe->ngroups <= 1) return 0;
-  // every other device group's verdict (system-scope loads of their words)
+  // every other device group's verdict (system-scope loads of their words).
+  // A group still undecided once the handshake bound has passed is decided
+  // for it: ABORT(W) by a compare-and-swap from its older word (round 6; the
+  // first CAS on a word wins, its own blocks included, so every group reads
+  // the same outcome), and every group reruns the window -- instead of the
+  // ~4 s spin ending in ST_FAULT when a peer's host drained late.
+  const int64_t gbound = bound < 0 ? 10000000 : bound;
   for (unsigned spins = 0;;) {
     bool dec = true, ab = false;
     if (lane < pe->ngroups) {
-      const gu64* w = (const gu64*)pe->ratio[pe->gleader[lane]] +
-                      (size_t)(HS_PLANE_SHARD + 1) * CHAIN_SH_SLOTS;
-      const unsigned long long x = g_load<true>(w);
-      const int32_t d = epoch_diff((uint32_t)(x >> 8), W);
+      gu64* w = (gu64*)pe->ratio[pe->gleader[lane]] + (size_t)(HS_PLANE_SHARD + 1) * CHAIN_SH_SLOTS;
+      unsigned long long x = g_load<true>(w);
+      int32_t d = epoch_diff((uint32_t)(x >> 8), W);
+      if (d < 0 && (int64_t)(__builtin_amdgcn_s_memrealtime() - t0) > gbound) {
+        const unsigned long long want = ((unsigned long long)W << 8) | 2u;
+        if (__hip_atomic_compare_exchange_strong(w, &x, want, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_SYSTEM))
+          x = want;
+        d = epoch_diff((uint32_t)(x >> 8), W);
+      }
       dec = d >= 0;
       ab = d > 0 || (d == 0 && (x & 0xffu) == 2u);
     }

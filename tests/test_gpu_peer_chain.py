@@ -588,7 +588,12 @@ def test_full_pool_falls_back_to_rccl_on_a_comm_shard():
     # groups' verdicts must agree on every aborted and every run window
     ["--rows", "300", "--cols", "500", "--window", "4", "--pivots", "400",
      "--abort-every", "3", "--run-pivots", "--late-drain", "0.6"],
-], ids=["solve", "push", "aborts_late_drain"])
+    # a drain 5 s late, past the ~4 s spin that ended in ST_FAULT before round
+    # 6: the early group now aborts the late group's undecided window by CAS
+    # after the 100-ms handshake bound, and both rerun until it catches up
+    ["--rows", "300", "--cols", "500", "--window", "4", "--pivots", "400",
+     "--abort-every", "3", "--run-pivots", "--late-drain", "5"],
+], ids=["solve", "push", "aborts_late_drain", "late_drain_past_spin_bound"])
 def test_peer_chain_device_groups_on_one_gpu(args):
     """The start handshake of ranks on DIFFERENT GPUs (device groups: each
     group settles its own arrivals, then waits for every other group's verdict
