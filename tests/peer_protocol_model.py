@@ -26,6 +26,11 @@ its hazards can be exercised on a CPU:
     64 lanes x RPL records (RPL = 1, 2, 4, 8; clamped indices), which covers
     every slot only while nr * B <= CHAIN_SH_SLOTS = 512 (config 4: 8 ranks x
     64 blocks is exactly that);
+  * device groups (round 6, `groups=`): ranks on different GPUs each settle
+    their own group's arrivals and verdict, then wait for every other group's
+    verdict; a group still undecided after the handshake bound is decided
+    ABORT(W) by a compare-and-swap on its word (mutant `no_group_cas`: the
+    round-5 wait, which runs into the spin bound when a group is late);
   * the owner-push row transport (round 5, `push=True`): the leaving row's
     owner writes its stale values into every peer's inbox (tagged granules, two
     halves by pivot parity) instead of every peer reading the owner's rows; the
@@ -85,8 +90,12 @@ def poll_slots(BR):
 class Device:
     """What every rank can reach: its peers' record buffers and stale rows."""
 
-    def __init__(self, nr, B, mutant=(), push=False):
+    def __init__(self, nr, B, mutant=(), push=False, groups=None):
         self.nr, self.B, self.mutant, self.push = nr, B, set(mutant), push
+        # device group of each rank (ranks sharing a GPU); one group by default
+        self.group_of = list(groups) if groups is not None else [0] * nr
+        self.ngroups = max(self.group_of) + 1
+        self.verdicts = [(0, 0)] * self.ngroups
         halves = 1 if "one_half" in self.mutant else 2
         self.slots = poll_slots(nr * B)
         assert self.slots == list(range(nr * B)), "the poll misses a record slot"
@@ -96,7 +105,6 @@ class Device:
         self.enter = [dict() for _ in range(nr)]
         self.done = [dict() for _ in range(nr)]
         self.arrive = {}
-        self.verdict = (0, 0)
         self.cas = threading.Lock()
         self.A = [None] * nr       # each rank's stale rows (read by peers' row gathers)
         self.row0 = [0] * nr
@@ -239,32 +247,61 @@ class Rank:
         return min(cand, key=lambda j: (o[j], j))
 
     def _start(self, b, W):
-        """chain_start: arrival granule, bounded wait for the group, then the
-        verdict by compare-and-swap (first writer for window W wins)."""
+        """chain_start: arrival granule, bounded wait for my device group, its
+        verdict by compare-and-swap (first writer for window W wins), then --
+        ranks on several GPUs -- every other group's verdict."""
         dev = self.dev
+        g = dev.group_of[self.rank]
         slot = self.rank * dev.B + b
         time.sleep(self.late(W, b))
         dev.arrive[slot] = _tag(W, 0, START)
         t0 = time.monotonic()
         want = GO
-        nxt, n = 0, dev.nr * dev.B  # (arrivals seen are not re-read: see _wait_all)
+        mine = [r * dev.B + x for r in range(dev.nr) if dev.group_of[r] == g
+                for x in range(dev.B)]
+        nxt, n = 0, len(mine)  # (arrivals seen are not re-read: see _wait_all)
         while True:
-            while nxt < n and dev.arrive.get(nxt) == _tag(W, 0, START):
+            while nxt < n and dev.arrive.get(mine[nxt]) == _tag(W, 0, START):
                 nxt += 1
-            if nxt == n and all(dev.arrive.get(x) == _tag(W, 0, START) for x in range(n)):
+            if nxt == n and all(dev.arrive.get(x) == _tag(W, 0, START) for x in mine):
                 break
+            if dev.verdicts[g][0] >= W:
+                break  # (the group's word already holds W: decided)
             if time.monotonic() - t0 > self.hs_bound:
                 want = ABORT
                 break
             time.sleep(POLL_SLEEP)
         with dev.cas:
-            vw, vs = dev.verdict
+            vw, vs = dev.verdicts[g]
             if vw > W:
                 return ABORT  # the group is past W: W was aborted
             if vw < W:
-                dev.verdict = (W, want)
-                return want
+                dev.verdicts[g] = (W, want)
+                vs = want
+        if vs != GO or dev.ngroups == 1:
             return vs
+        # every other group's verdict; an undecided one is aborted by CAS once
+        # the handshake bound has passed (round 6; spx_chain.hpp chain_start)
+        t_end = time.monotonic() + WAIT_LIMIT
+        while True:
+            dec, ab = True, False
+            for h in range(dev.ngroups):
+                vw, vs = dev.verdicts[h]
+                if (vw < W and "no_group_cas" not in dev.mutant
+                        and time.monotonic() - t0 > self.hs_bound):
+                    with dev.cas:
+                        if dev.verdicts[h][0] < W:
+                            dev.verdicts[h] = (W, ABORT)
+                        vw, vs = dev.verdicts[h]
+                dec &= vw >= W
+                ab |= vw > W or (vw == W and vs == ABORT)
+            if ab:
+                return ABORT
+            if dec:
+                return GO
+            if time.monotonic() > t_end:
+                raise Timeout(f"rank {self.rank}: other groups' verdicts for window {W}")
+            time.sleep(POLL_SLEEP)
 
     def _block(self, b, W, it0, npiv, cpb, rpb, c0, stop0, sh, obj_new, lock):
         dev, B, N, nr, rank = self.dev, self.dev.B, self.N, self.dev.nr, self.rank

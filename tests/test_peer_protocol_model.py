@@ -21,15 +21,17 @@ from oracle import simplex_oracle as O
 
 
 def _run(world=2, B=2, kind="dense", m=20, n=14, seed=3, K=4, rule="dantzig", mutant=(),
-         delay=None, late=None, max_iters=10 ** 6, hs_bound=0.5, stop_after=None, push=False):
+         delay=None, late=None, max_iters=10 ** 6, hs_bound=0.5, stop_after=None, push=False,
+         groups=None, late_rank=None):
     from simplex_amd import synth
     from simplex_amd.dist import row_partition
-    dev = M.Device(world, B, mutant, push=push)
+    dev = M.Device(world, B, mutant, push=push, groups=groups)
     ranks = []
     for r in range(world):
         r0, r1 = row_partition(m, world, r)
         T, obj, basis = synth.tableau_rows(kind, m, n, seed, r0, r1, order="C")
-        ranks.append(M.Rank(dev, r, T, obj, basis, r0, K, rule, delay=delay, late=late,
+        lt = late_rank.get(r) if late_rank else late
+        ranks.append(M.Rank(dev, r, T, obj, basis, r0, K, rule, delay=delay, late=lt,
                             hs_bound=hs_bound))
     errs, res = [], {}
 
@@ -240,3 +242,40 @@ def test_model_push_needs_no_window_end_barrier():
                             mutant=("no_done_barrier",))
     assert not errs, errs
     _check(ranks, res, "dense", m, n, 3, "dantzig")
+
+
+# ---- device groups (ranks on different GPUs; round 6) -----------------------
+
+@pytest.mark.parametrize("groups", [[0, 1], [0, 1, 2], [0, 0, 1]], ids=["2x1", "3x1", "2+1"])
+def test_model_device_groups_bit_exact(groups):
+    """Each device group settles its own start handshake, then waits for every
+    other group's verdict (chain_start's cross-group stage): under jitter, with
+    one to two ranks per group, every rank equals the oracle."""
+    world = len(groups)
+    ranks, res, errs = _run(world=world, B=2, m=24, n=16, seed=5, K=4, groups=groups,
+                            delay=_jitter(11))
+    assert not errs, errs
+    _check(ranks, res, "dense", 24, 16, 5, "dantzig")
+
+
+def _late_first_window(seconds):
+    def late(W, b):
+        return seconds if W == 1 else 0.0
+    return late
+
+
+def test_model_late_device_group_is_aborted_by_cas():
+    """A group whose ranks reach the first window later than the spin bound
+    (WAIT_LIMIT, the kernels' ~4 s; here 6 s): the early group, having said
+    GO, decides the late group's window ABORT by CAS once the handshake bound
+    passed, and both rerun until the late one catches up -- bit-exact, with
+    reruns on every rank.  Without the CAS (mutant), the early group's wait
+    runs into the bound (the round-5 ST_FAULT)."""
+    kw = dict(world=2, B=2, m=20, n=14, seed=3, K=4, groups=[0, 1], hs_bound=0.2,
+              late_rank={1: _late_first_window(6.0)})
+    ranks, res, errs = _run(**kw)
+    assert not errs, errs
+    _check(ranks, res, "dense", 20, 14, 3, "dantzig")
+    assert all(rk.reruns > 0 for rk in ranks), [rk.reruns for rk in ranks]
+    ranks, res, errs = _run(mutant=("no_group_cas",), **kw)
+    assert errs and all(isinstance(e, M.Timeout) for e in errs), errs
